@@ -1,0 +1,184 @@
+/*
+ * swarm_mi355x.h — C-ABI of the MI355X-native vectorised drone-swarm step/observe/reward path.
+ *
+ * One call steps E independent swarm envs of N drones on the GPU (gfx950).  It replaces the
+ * reference's per-env Python hot path:
+ *
+ *   swarm_step    <- DroneSwarmEnv.step            src/swarm_marl/envs/drone_swarm_env.py:92-174
+ *                    (+ _clip_speed :179-183, _collision_mask :185-208,
+ *                     _formation_penalties :210-224, _build_obs :226-243,
+ *                     _nearest_neighbor_features :245-271, _nearest_obstacle_features :273-291,
+ *                     _global_state :293-302)
+ *                 <- DronePhysicsEnv.step          src/swarm_marl/envs/drone_physics_env.py:279-419
+ *                    (point-mass restatement of the PyBullet force/substep loop :320-360,
+ *                     _get_obs :421-462, _get_infos :540-583)
+ *   swarm_reset   <- DroneSwarmEnv.reset           drone_swarm_env.py:65-90 (device RNG draws;
+ *                    the seeded NumPy-stream reset stays on the host and uses swarm_observe)
+ *                 <- DronePhysicsEnv.reset         drone_physics_env.py:174-263
+ *   swarm_observe <- the observation/info half of reset(): drone_swarm_env.py:82-90
+ *                    (_build_obs for every agent, distance_to_goal, global_state)
+ *
+ * Conventions
+ *  - Every buffer is device memory owned by the caller (PyTorch tensors in the Python host
+ *    package).  All buffers are dense, C-contiguous, and must not overlap each other.
+ *  - Calls are asynchronous on `hip_stream` (a hipStream_t; NULL = the null stream).  No
+ *    allocation, no host synchronisation, no exceptions cross the ABI: 0 on success, a negative
+ *    SWARM_E* code otherwise; swarm_last_error() gives a thread-local message.
+ *  - Reentrant for distinct state/out buffers.
+ */
+#ifndef SWARM_MI355X_H
+#define SWARM_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SWARM_ABI_VERSION 1
+
+/* error codes */
+#define SWARM_OK 0
+#define SWARM_EINVAL -1    /* bad argument / unsupported configuration */
+#define SWARM_ENULL -2     /* required pointer is NULL */
+#define SWARM_ELIMIT -3    /* size exceeds a documented limit (N, K, Ms, LDS budget) */
+#define SWARM_EHIP -4      /* HIP launch / runtime error */
+
+/* dynamics modes */
+#define SWARM_DYN_KINEMATIC 0         /* DroneSwarmEnv Euler integrator (drone_swarm_env.py:103-117) */
+#define SWARM_DYN_POINTMASS_PHYSICS 1 /* DronePhysicsEnv force model as a point mass (drone_physics_env.py:320-360) */
+
+/* reward modes */
+#define SWARM_REW_SWARM 0    /* progress + formation + goal + collision (drone_swarm_env.py:137-172) */
+#define SWARM_REW_PHYSICS 1  /* -0.1*dist, -10 collision, +50 goal (drone_physics_env.py:374-417) */
+
+/* env_done bits ([E] u8) */
+#define SWARM_ENV_TERMINATED 1u  /* terminated["__all__"] */
+#define SWARM_ENV_TRUNCATED 2u   /* truncated["__all__"] */
+#define SWARM_ENV_RESET 4u       /* the env was auto-reset in this call; obs/state are the new episode's */
+
+/* info_flags bits ([E,N] u8) */
+#define SWARM_AGENT_STEPPED 1u    /* agent had a reward/terminated/truncated entry this step */
+#define SWARM_AGENT_REACHED 2u    /* infos["reached_goal"] */
+#define SWARM_AGENT_COLLISION 4u  /* infos["collision"] */
+#define SWARM_AGENT_HAS_OBS 8u    /* obs/infos entry emitted by the dict API (continuing agent) */
+
+/*
+ * Environment parameters.  Field meaning follows DroneEnvConfig (src/swarm_marl/envs/common.py:7-25)
+ * plus `num_drones` (drone_swarm_env.py:32-34); floating fields are the Python (double) values,
+ * the library derives the float32 constants the reference's NumPy code actually compares against.
+ */
+typedef struct swarm_params {
+  int32_t abi_version;       /* must be SWARM_ABI_VERSION */
+  int32_t num_envs;          /* E (local shard) */
+  int32_t num_drones;        /* N, 1..1024 */
+  int32_t num_obstacles;     /* M >= 0 */
+  int32_t sensed_obstacles;  /* Ms (<= 16 supported); <= 0 -> no obstacle block in obs */
+  int32_t neighbor_k;        /* K (<= 16 supported); <= 0 -> no neighbour block in obs */
+  int32_t max_steps;
+  int32_t dynamics;          /* SWARM_DYN_* */
+  int32_t reward_mode;       /* SWARM_REW_* */
+  int32_t auto_reset;        /* swarm_step: reset envs whose episode ended, in-kernel (device RNG) */
+  int32_t physics_substeps;  /* physics: int(dt*240) (drone_physics_env.py:323) */
+  int32_t damping_law;       /* physics: 0 = btMultiBody -d*(1+|v|)*v (default), 1 = btRigidBody v*=(1-d)^h */
+  int64_t env_offset;        /* global index of local env 0 (RNG key; sharding across ranks) */
+  uint64_t seed;             /* device-RNG key */
+  double world_size;
+  double dt;
+  double max_speed;
+  double max_accel;
+  double collision_radius;
+  double goal_radius;
+  double obstacle_radius;
+  double desired_spacing;
+  double reward_progress_scale;
+  double reward_goal;
+  double reward_collision;
+  double reward_formation_scale;
+  /* physics-mode constants (drone_physics_env.py:135,343; drone.urdf geometry) */
+  double gravity;            /* -9.81 */
+  double gravity_comp;       /* 9.5 */
+  double substep_dt;         /* 1/240 */
+  double drone_contact_radius;    /* contact approximation radius of the 0.3x0.3x0.05 box */
+  double ground_contact_height;   /* z at or below which the box touches the plane */
+} swarm_params_t;
+
+/* Per-env state, device SoA blocks (all dense, C-contiguous). */
+typedef struct swarm_state {
+  float* pos;          /* [E,N,3] */
+  float* vel;          /* [E,N,3] */
+  float* goal;         /* [E,3] */
+  float* obstacles;    /* [E,M,3] (may be NULL iff M == 0) */
+  uint8_t* active;     /* [E,N]  agent still in env.agents */
+  int32_t* step_count; /* [E] */
+  uint32_t* episode;   /* [E]  device-RNG episode counter (incremented by every device reset) */
+  float* damping;      /* [E,N] physics linear damping (NULL allowed in kinematic mode) */
+} swarm_state_t;
+
+/* Outputs.  Optional pointers may be NULL. */
+typedef struct swarm_out {
+  float* obs;            /* [E,N,D], D = 9 + 4*max(K,0) + 4*max(Ms,0) */
+  float* reward;         /* [E,N]   (0 for agents without a reward entry) */
+  uint8_t* terminated;   /* [E,N] */
+  uint8_t* truncated;    /* [E,N] */
+  uint8_t* env_done;     /* [E]     SWARM_ENV_* bits */
+  float* dist_goal;      /* [E,N]   optional: infos["distance_to_goal"] */
+  uint8_t* info_flags;   /* [E,N]   optional: SWARM_AGENT_* bits */
+  float* global_state;   /* [E,6N+3] optional: concat(pos, vel, goal) (drone_swarm_env.py:293-302) */
+} swarm_out_t;
+
+/* Launch geometry actually used (for tests / profiling). */
+typedef struct swarm_launch_info {
+  int32_t threads_per_block;
+  int32_t envs_per_block;
+  int32_t lanes_per_env;
+  int32_t blocks;
+  int32_t lds_bytes;
+  int32_t neighbor_slots;   /* compile-time top-K slots of the chosen kernel variant */
+  int32_t obstacle_slots;
+  int32_t obs_dim;
+  int32_t staged_obs;       /* 1: obs staged through LDS and stored coalesced */
+} swarm_launch_info_t;
+
+int swarm_abi_version(void);
+const char* swarm_last_error(void);
+
+/* Fill swarm_params_t with DroneEnvConfig defaults (common.py:9-24), num_drones = 3. */
+void swarm_params_default(swarm_params_t* p);
+
+/* Observation width D for `p` (drone_swarm_env.py:41-45). */
+int swarm_obs_dim(const swarm_params_t* p);
+
+/* Geometry of the kernel `swarm_step` would launch for `p`. */
+int swarm_query_launch(const swarm_params_t* p, swarm_launch_info_t* info);
+
+/*
+ * One env step for every env: integrate, clip, distances, collision, formation, rewards,
+ * terminations, (auto-reset), kNN observation, optional infos/global_state.
+ * actions: [E,N,3] f32.  action_mask: [E,N] u8 or NULL (= every agent supplied an action;
+ * a missing action is a zero action in swarm mode, no thrust in physics mode).
+ * obs/global_state describe the state AFTER the call (post-reset for auto-reset envs).
+ */
+int swarm_step(const swarm_params_t* p, const swarm_state_t* s, const float* actions,
+               const uint8_t* action_mask, const swarm_out_t* o, void* hip_stream);
+
+/*
+ * Device reset: draw a new episode (Philox4x32-10 keyed by seed, global env index and
+ * episode counter) for the envs with env_mask[e] != 0 (NULL = all) and write their obs,
+ * dist_goal, global_state.  Outputs of envs not in the mask are left untouched.
+ */
+int swarm_reset(const swarm_params_t* p, const swarm_state_t* s, const uint8_t* env_mask,
+                const swarm_out_t* o, void* hip_stream);
+
+/*
+ * Observation only: obs / dist_goal / global_state for the current state of the masked envs
+ * (NULL = all).  The state is not modified.  Used after a host-side seeded reset.
+ */
+int swarm_observe(const swarm_params_t* p, const swarm_state_t* s, const uint8_t* env_mask,
+                  const swarm_out_t* o, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SWARM_MI355X_H */

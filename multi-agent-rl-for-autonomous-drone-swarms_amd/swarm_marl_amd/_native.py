@@ -1,0 +1,151 @@
+"""ctypes binding of the C-ABI in include/swarm_mi355x.h (libswarm_mi355x.so, built for gfx950).
+
+The library is the product's compute path: there is no CPU fallback.  If it is missing the
+import of the engine fails loudly (NativeLibraryError) — build it with
+`python -c "import __graft_entry__ as g; g.build()"` from the repository root.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+LIB_NAME = "libswarm_mi355x.so"
+LIB_DIR = Path(__file__).resolve().parent / "_lib"
+LIB_PATH = LIB_DIR / LIB_NAME
+
+ABI_VERSION = 1
+
+SWARM_OK = 0
+SWARM_EINVAL = -1
+SWARM_ENULL = -2
+SWARM_ELIMIT = -3
+SWARM_EHIP = -4
+
+DYN_KINEMATIC = 0
+DYN_POINTMASS_PHYSICS = 1
+REW_SWARM = 0
+REW_PHYSICS = 1
+
+ENV_TERMINATED = 1
+ENV_TRUNCATED = 2
+ENV_RESET = 4
+
+AGENT_STEPPED = 1
+AGENT_REACHED = 2
+AGENT_COLLISION = 4
+AGENT_HAS_OBS = 8
+
+# every symbol include/swarm_mi355x.h declares
+EXPORTED_SYMBOLS = (
+    "swarm_abi_version", "swarm_last_error", "swarm_params_default", "swarm_obs_dim",
+    "swarm_query_launch", "swarm_step", "swarm_reset", "swarm_observe",
+)
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class SwarmParams(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", ctypes.c_int32),
+        ("num_envs", ctypes.c_int32),
+        ("num_drones", ctypes.c_int32),
+        ("num_obstacles", ctypes.c_int32),
+        ("sensed_obstacles", ctypes.c_int32),
+        ("neighbor_k", ctypes.c_int32),
+        ("max_steps", ctypes.c_int32),
+        ("dynamics", ctypes.c_int32),
+        ("reward_mode", ctypes.c_int32),
+        ("auto_reset", ctypes.c_int32),
+        ("physics_substeps", ctypes.c_int32),
+        ("damping_law", ctypes.c_int32),
+        ("env_offset", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+        ("world_size", ctypes.c_double),
+        ("dt", ctypes.c_double),
+        ("max_speed", ctypes.c_double),
+        ("max_accel", ctypes.c_double),
+        ("collision_radius", ctypes.c_double),
+        ("goal_radius", ctypes.c_double),
+        ("obstacle_radius", ctypes.c_double),
+        ("desired_spacing", ctypes.c_double),
+        ("reward_progress_scale", ctypes.c_double),
+        ("reward_goal", ctypes.c_double),
+        ("reward_collision", ctypes.c_double),
+        ("reward_formation_scale", ctypes.c_double),
+        ("gravity", ctypes.c_double),
+        ("gravity_comp", ctypes.c_double),
+        ("substep_dt", ctypes.c_double),
+        ("drone_contact_radius", ctypes.c_double),
+        ("ground_contact_height", ctypes.c_double),
+    ]
+
+
+class SwarmState(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name in
+                ("pos", "vel", "goal", "obstacles", "active", "step_count", "episode", "damping")]
+
+
+class SwarmOut(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name in
+                ("obs", "reward", "terminated", "truncated", "env_done", "dist_goal",
+                 "info_flags", "global_state")]
+
+
+class SwarmLaunchInfo(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_int32) for name in
+                ("threads_per_block", "envs_per_block", "lanes_per_env", "blocks", "lds_bytes",
+                 "neighbor_slots", "obstacle_slots", "obs_dim", "staged_obs")]
+
+
+_LIB = None
+
+
+def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
+    """Load libswarm_mi355x.so (once) and declare its signatures."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = Path(path) if path is not None else LIB_PATH
+    if not p.exists():
+        raise NativeLibraryError(
+            f"{p} is missing: the MI355X swarm engine has no CPU fallback. Build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` in the repository root.")
+    lib = ctypes.CDLL(str(p))
+    P, S, O = ctypes.POINTER(SwarmParams), ctypes.POINTER(SwarmState), ctypes.POINTER(SwarmOut)
+    vp = ctypes.c_void_p
+    lib.swarm_abi_version.restype = ctypes.c_int
+    lib.swarm_abi_version.argtypes = []
+    lib.swarm_last_error.restype = ctypes.c_char_p
+    lib.swarm_last_error.argtypes = []
+    lib.swarm_params_default.restype = None
+    lib.swarm_params_default.argtypes = [P]
+    lib.swarm_obs_dim.restype = ctypes.c_int
+    lib.swarm_obs_dim.argtypes = [P]
+    lib.swarm_query_launch.restype = ctypes.c_int
+    lib.swarm_query_launch.argtypes = [P, ctypes.POINTER(SwarmLaunchInfo)]
+    lib.swarm_step.restype = ctypes.c_int
+    lib.swarm_step.argtypes = [P, S, vp, vp, O, vp]
+    lib.swarm_reset.restype = ctypes.c_int
+    lib.swarm_reset.argtypes = [P, S, vp, O, vp]
+    lib.swarm_observe.restype = ctypes.c_int
+    lib.swarm_observe.argtypes = [P, S, vp, O, vp]
+    got = lib.swarm_abi_version()
+    if got != ABI_VERSION:
+        raise NativeLibraryError(f"{p}: ABI version {got}, expected {ABI_VERSION}")
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def check(rc: int, lib: ctypes.CDLL | None = None) -> None:
+    """Raise on a negative return code (bad arguments -> ValueError, HIP errors -> RuntimeError)."""
+    if rc == SWARM_OK:
+        return
+    lib = lib or load_library()
+    msg = (lib.swarm_last_error() or b"").decode(errors="replace")
+    if rc in (SWARM_EINVAL, SWARM_ENULL, SWARM_ELIMIT):
+        raise ValueError(f"swarm_mi355x error {rc}: {msg}")
+    raise RuntimeError(f"swarm_mi355x error {rc}: {msg}")

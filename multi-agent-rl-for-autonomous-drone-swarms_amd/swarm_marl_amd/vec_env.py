@@ -1,0 +1,231 @@
+"""VecSwarm — E independent swarm envs stepped by one HIP kernel launch per call.
+
+This is the throughput API the dict-API envs (envs/*.py) sit on.  All state and outputs are
+PyTorch tensors resident in HBM; a step is ONE asynchronous launch on the current HIP stream with
+no host synchronisation.  Output tensors are persistent buffers overwritten by the next call
+(clone them to keep them).
+
+Semantics per env follow DroneSwarmEnv.step (src/swarm_marl/envs/drone_swarm_env.py:92-174) in
+"kinematic" mode and DronePhysicsEnv.step (src/swarm_marl/envs/drone_physics_env.py:279-419,
+point-mass restatement) in "physics" mode.  With auto_reset=True an env whose episode ended is
+re-drawn in the same launch (Philox stream keyed by seed, global env index and episode number);
+`obs` then holds the new episode's first observation — the reference emits no terminal obs
+(drone_swarm_env.py:154), so nothing is lost.  env_done carries terminated/truncated["__all__"]
+and a RESET bit.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import asdict
+from typing import Any
+
+import torch
+
+from . import _native as nat
+from .envs.common import DroneEnvConfig
+
+PHYSICS_DEFAULTS = dict(gravity=-9.81, gravity_comp=9.5, substep_dt=1.0 / 240.0,
+                        drone_contact_radius=0.15, ground_contact_height=0.025, damping_law=0)
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+class VecSwarm:
+    def __init__(self, num_envs: int, config: dict[str, Any] | DroneEnvConfig | None = None, *,
+                 num_drones: int | None = None, dynamics: str = "kinematic",
+                 auto_reset: bool = True, seed: int = 0, env_offset: int = 0,
+                 device: str | torch.device | None = None, with_infos: bool = False,
+                 with_global_state: bool = False, physics: dict[str, Any] | None = None):
+        if isinstance(config, DroneEnvConfig):
+            cfg, raw = config, {}
+        else:
+            raw = dict(config or {})
+            cfg = DroneEnvConfig.from_dict({k: v for k, v in raw.items() if k != "num_drones"})
+        n = int(num_drones if num_drones is not None else raw.get("num_drones", 3))
+        if dynamics not in ("kinematic", "physics"):
+            raise ValueError(f"dynamics must be 'kinematic' or 'physics', got {dynamics!r}")
+        self.cfg = cfg
+        self.num_envs = int(num_envs)
+        self.num_drones = n
+        self.dynamics = dynamics
+        self.lib = nat.load_library()
+        if device is None:
+            if not torch.cuda.is_available():
+                raise RuntimeError("VecSwarm needs a ROCm GPU (gfx950); none is visible")
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("VecSwarm state must live on a GPU device ('cuda' on ROCm)")
+
+        phys = dict(PHYSICS_DEFAULTS)
+        phys.update(physics or {})
+        p = nat.SwarmParams()
+        self.lib.swarm_params_default(ctypes.byref(p))
+        p.num_envs = self.num_envs
+        p.num_drones = n
+        p.num_obstacles = int(cfg.num_obstacles)
+        p.sensed_obstacles = int(cfg.sensed_obstacles)
+        p.neighbor_k = int(cfg.neighbor_k)
+        p.max_steps = int(cfg.max_steps)
+        p.dynamics = nat.DYN_KINEMATIC if dynamics == "kinematic" else nat.DYN_POINTMASS_PHYSICS
+        p.reward_mode = nat.REW_SWARM if dynamics == "kinematic" else nat.REW_PHYSICS
+        p.auto_reset = 1 if auto_reset else 0
+        p.physics_substeps = int(phys.get("substeps", int(float(cfg.dt) * 240)))  # :323
+        p.damping_law = int(phys["damping_law"])
+        p.env_offset = int(env_offset)
+        p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        for name in ("world_size", "dt", "max_speed", "max_accel", "collision_radius",
+                     "goal_radius", "obstacle_radius", "desired_spacing", "reward_progress_scale",
+                     "reward_goal", "reward_collision", "reward_formation_scale"):
+            setattr(p, name, float(getattr(cfg, name)))
+        for name in ("gravity", "gravity_comp", "substep_dt", "drone_contact_radius",
+                     "ground_contact_height"):
+            setattr(p, name, float(phys[name]))
+        self.params = p
+        self.launch_info = nat.SwarmLaunchInfo()
+        nat.check(self.lib.swarm_query_launch(ctypes.byref(p), ctypes.byref(self.launch_info)),
+                  self.lib)
+        self.obs_dim = int(self.lib.swarm_obs_dim(ctypes.byref(p)))
+
+        e, m, d = self.num_envs, int(cfg.num_obstacles), self.obs_dim
+        kw = dict(device=self.device)
+        f32 = torch.float32
+        # ---- state (SoA blocks, [E, ...] contiguous)
+        self.pos = torch.zeros((e, n, 3), dtype=f32, **kw)
+        self.vel = torch.zeros((e, n, 3), dtype=f32, **kw)
+        self.goal = torch.zeros((e, 3), dtype=f32, **kw)
+        self.obstacles = torch.zeros((e, m, 3), dtype=f32, **kw)
+        self.active = torch.ones((e, n), dtype=torch.bool, **kw)
+        self.step_count = torch.zeros((e,), dtype=torch.int32, **kw)
+        self.episode = torch.zeros((e,), dtype=torch.int32, **kw)  # read as uint32 by the kernel
+        self.damping = torch.zeros((e, n), dtype=f32, **kw)
+        # ---- outputs (persistent buffers)
+        self.obs = torch.zeros((e, n, d), dtype=f32, **kw)
+        self.reward = torch.zeros((e, n), dtype=f32, **kw)
+        self.terminated = torch.zeros((e, n), dtype=torch.bool, **kw)
+        self.truncated = torch.zeros((e, n), dtype=torch.bool, **kw)
+        self.env_done = torch.zeros((e,), dtype=torch.uint8, **kw)
+        self.dist_goal = torch.zeros((e, n), dtype=f32, **kw) if with_infos else None
+        self.info_flags = torch.zeros((e, n), dtype=torch.uint8, **kw) if with_infos else None
+        self.global_state = (torch.zeros((e, 6 * n + 3), dtype=f32, **kw)
+                             if with_global_state else None)
+        self._bind()
+
+    # ------------------------------------------------------------------ plumbing
+    def _bind(self) -> None:
+        s = nat.SwarmState()
+        s.pos, s.vel, s.goal = _ptr(self.pos), _ptr(self.vel), _ptr(self.goal)
+        s.obstacles = _ptr(self.obstacles) if self.obstacles.numel() else None
+        s.active, s.step_count = _ptr(self.active), _ptr(self.step_count)
+        s.episode, s.damping = _ptr(self.episode), _ptr(self.damping)
+        o = nat.SwarmOut()
+        o.obs, o.reward = _ptr(self.obs), _ptr(self.reward)
+        o.terminated, o.truncated = _ptr(self.terminated), _ptr(self.truncated)
+        o.env_done = _ptr(self.env_done)
+        o.dist_goal, o.info_flags = _ptr(self.dist_goal), _ptr(self.info_flags)
+        o.global_state = _ptr(self.global_state)
+        self._state_c, self._out_c = s, o
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _check_tensor(self, name: str, t: torch.Tensor, shape: tuple, dtype) -> None:
+        if not isinstance(t, torch.Tensor):
+            raise ValueError(f"{name} must be a torch.Tensor")
+        if t.device != self.device:
+            raise ValueError(f"{name} is on {t.device}, expected {self.device}")
+        if t.dtype != dtype:
+            raise ValueError(f"{name} has dtype {t.dtype}, expected {dtype}")
+        if tuple(t.shape) != tuple(shape):
+            raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+
+    def _mask_ptr(self, env_mask) -> int | None:
+        if env_mask is None:
+            return None
+        mk = env_mask
+        if mk.dtype != torch.uint8:
+            mk = mk.to(torch.uint8)
+        self._check_tensor("env_mask", mk, (self.num_envs,), torch.uint8)
+        self._keep = mk
+        return mk.data_ptr()
+
+    # ------------------------------------------------------------------ API
+    def step(self, actions: torch.Tensor, action_mask: torch.Tensor | None = None):
+        """One step of all envs.  actions [E,N,3] float32 on the device.
+
+        Returns (obs [E,N,D], reward [E,N] f32, terminated [E,N] bool, truncated [E,N] bool,
+        env_done [E] u8 bits).  Views into persistent buffers.
+        """
+        self._check_tensor("actions", actions, (self.num_envs, self.num_drones, 3), torch.float32)
+        am = None
+        if action_mask is not None:
+            if action_mask.dtype == torch.bool:
+                action_mask = action_mask.view(torch.uint8)
+            self._check_tensor("action_mask", action_mask, (self.num_envs, self.num_drones),
+                               torch.uint8)
+            am = action_mask.data_ptr()
+        rc = self.lib.swarm_step(ctypes.byref(self.params), ctypes.byref(self._state_c),
+                                 actions.data_ptr(), am, ctypes.byref(self._out_c), self._stream())
+        nat.check(rc, self.lib)
+        return self.obs, self.reward, self.terminated, self.truncated, self.env_done
+
+    def reset(self, env_mask: torch.Tensor | None = None) -> torch.Tensor:
+        """Device reset (Philox draws) of the masked envs (all if None); returns obs."""
+        rc = self.lib.swarm_reset(ctypes.byref(self.params), ctypes.byref(self._state_c),
+                                  self._mask_ptr(env_mask), ctypes.byref(self._out_c),
+                                  self._stream())
+        nat.check(rc, self.lib)
+        return self.obs
+
+    def observe(self, env_mask: torch.Tensor | None = None) -> torch.Tensor:
+        """obs / dist_goal / global_state of the current state (no state change)."""
+        rc = self.lib.swarm_observe(ctypes.byref(self.params), ctypes.byref(self._state_c),
+                                    self._mask_ptr(env_mask), ctypes.byref(self._out_c),
+                                    self._stream())
+        nat.check(rc, self.lib)
+        return self.obs
+
+    def set_state(self, *, pos=None, vel=None, goal=None, obstacles=None, active=None,
+                  step_count=None, episode=None, damping=None) -> None:
+        """Inject state (host or device arrays); shapes as the state tensors."""
+        for name, val in (("pos", pos), ("vel", vel), ("goal", goal), ("obstacles", obstacles),
+                          ("active", active), ("step_count", step_count),
+                          ("episode", episode), ("damping", damping)):
+            if val is None:
+                continue
+            dst = getattr(self, name)
+            src = torch.as_tensor(val)
+            if tuple(src.shape) != tuple(dst.shape):
+                raise ValueError(f"{name}: shape {tuple(src.shape)} != {tuple(dst.shape)}")
+            dst.copy_(src.to(dtype=dst.dtype), non_blocking=False)
+
+    def state_dict(self) -> dict[str, torch.Tensor]:
+        return dict(pos=self.pos, vel=self.vel, goal=self.goal, obstacles=self.obstacles,
+                    active=self.active, step_count=self.step_count, episode=self.episode,
+                    damping=self.damping)
+
+    @property
+    def config(self) -> dict[str, Any]:
+        d = asdict(self.cfg)
+        d["num_drones"] = self.num_drones
+        return d
+
+    def algorithmic_bytes_per_step(self) -> int:
+        """HBM bytes one step must move: per agent action 12 + pos/vel r/w 48 +
+        active r/w 2 + obs 4D + reward 4 + terminated/truncated 2; per env goal 12 + obstacles
+        12M + step r/w 8 + env_done 1 (+ optional infos / global_state)."""
+        n, e, d, m = self.num_drones, self.num_envs, self.obs_dim, int(self.cfg.num_obstacles)
+        per_agent = 12 + 48 + 2 + 4 * d + 4 + 2
+        per_env = 12 + 12 * m + 8 + 1
+        extra = 0
+        if self.dist_goal is not None:
+            per_agent += 5
+        if self.global_state is not None:
+            extra = e * (6 * n + 3) * 4
+        if self.dynamics == "physics":
+            per_agent += 4
+        return e * (n * per_agent + per_env) + extra
