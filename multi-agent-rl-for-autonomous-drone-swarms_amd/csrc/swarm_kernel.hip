@@ -57,6 +57,12 @@ struct KParams {
 };
 
 // ------------------------------------------------------------------ exact numerics
+// No FP contraction anywhere in this file (the reference's NumPy ops round every product).
+#pragma clang fp contract(off)
+// Correctly rounded square roots.  NB: HIP's __fsqrt_rn is v_sqrt_f32 (1 ulp) unless
+// OCML_BASIC_ROUNDED_OPERATIONS is defined; llvm.sqrt lowers to the IEEE-exact sequence.
+__device__ __forceinline__ float sqrt_rn(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ double dsqrt_rn(double x) { return __builtin_sqrt(x); }
 // np.linalg.norm(v) of a float32 3-vector: OpenBLAS sdot = double accumulation of float
 // products, rounded to float; sqrt in float.  Returns the float sum s (d = sqrtf(s)).
 __device__ __forceinline__ float sqsum_1d(float x, float y, float z) {
@@ -150,7 +156,7 @@ __device__ __forceinline__ void obstacle_pass(const float4* __restrict__ obst4, 
   for (int m = 0; m < M; ++m) {
     const float4 q = obst4[m];
     const float s = sqsum_axis(__fsub_rn(q.x, px), __fsub_rn(q.y, py), __fsub_rn(q.z, pz));
-    if constexpr (MSL > 0) topk_insert<MSL>(ok, make_key(__fsqrt_rn(s), m));
+    if constexpr (MSL > 0) topk_insert<MSL>(ok, make_key(sqrt_rn(s), m));
     if constexpr (COLL) coll = coll || (chk && (s <= s_thr));
   }
 }
@@ -220,7 +226,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     const bool has = (amask == nullptr) || (amask[ag] != 0);
     if constexpr (DYN == DYN_KIN) {
       if (act) {  // drone_swarm_env.py:98-111
-        prev_d = __fsqrt_rn(sqsum_1d(__fsub_rn(gx, px), __fsub_rn(gy, py), __fsub_rn(gz, pz)));
+        prev_d = sqrt_rn(sqsum_1d(__fsub_rn(gx, px), __fsub_rn(gy, py), __fsub_rn(gz, pz)));
         if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
         ax = __fmul_rn(fminf(fmaxf(ax, -1.f), 1.f), P.amax);
         ay = __fmul_rn(fminf(fmaxf(ay, -1.f), 1.f), P.amax);
@@ -228,7 +234,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         vx = __fadd_rn(vx, __fmul_rn(ax, P.dt));
         vy = __fadd_rn(vy, __fmul_rn(ay, P.dt));
         vz = __fadd_rn(vz, __fmul_rn(az, P.dt));
-        const float sp = __fsqrt_rn(sqsum_1d(vx, vy, vz));  // _clip_speed :179-183
+        const float sp = sqrt_rn(sqsum_1d(vx, vy, vz));  // _clip_speed :179-183
         if (!(sp <= P.vmax || sp < P.eps_speed)) {
           vx = __fmul_rn(__fdiv_rn(vx, sp), P.vmax);
           vy = __fmul_rn(__fdiv_rn(vy, sp), P.vmax);
@@ -253,14 +259,14 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       float fac = 1.f;
       if (P.damping_law == 1) fac = __double2float_rn(pow((double)__fsub_rn(1.f, damp), (double)h));
       for (int s = 0; s < P.substeps; ++s) {
-        const float sp = __fsqrt_rn(sqsum_1d(vx, vy, vz));
+        const float sp = sqrt_rn(sqsum_1d(vx, vy, vz));
         if (has && sp > P.vmax) {
           vx = __fmul_rn(__fdiv_rn(vx, sp), P.vmax);
           vy = __fmul_rn(__fdiv_rn(vy, sp), P.vmax);
           vz = __fmul_rn(__fdiv_rn(vz, sp), P.vmax);
         }
         if (P.damping_law == 0) {
-          const float sp2 = __fsqrt_rn(sqsum_1d(vx, vy, vz));
+          const float sp2 = sqrt_rn(sqsum_1d(vx, vy, vz));
           const float c = __fmul_rn(damp, __fadd_rn(1.f, sp2));
           vx = __fadd_rn(vx, __fmul_rn(h, __fsub_rn(cx, __fmul_rn(c, vx))));
           vy = __fadd_rn(vy, __fmul_rn(h, __fsub_rn(cy, __fmul_rn(c, vy))));
@@ -347,7 +353,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   if (mode == MODE_STEP) {
     if (is_agent) {
       if constexpr (DYN == DYN_KIN) {
-        const float curr = __fsqrt_rn(sqsum_1d(__fsub_rn(gx, px), __fsub_rn(gy, py), __fsub_rn(gz, pz)));
+        const float curr = sqrt_rn(sqsum_1d(__fsub_rn(gx, px), __fsub_rn(gy, py), __fsub_rn(gz, pz)));
         dist_out = curr;
         if (act) {
           reached = (double)curr <= P.goal_radius;  // fp64 compare, :124-127
@@ -364,7 +370,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         const double dx = __dsub_rn((double)px, (double)gx);
         const double dy = __dsub_rn((double)py, (double)gy);
         const double dz = __dsub_rn((double)pz, (double)gz);
-        dist_phys = __dsqrt_rn(__dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)));
+        dist_phys = dsqrt_rn(__dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)));
         dist_out = __double2float_rn(dist_phys);
         collided = coll || (pz <= P.ground_z);
         reached = dist_phys < P.goal_radius;
@@ -452,7 +458,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       }
     }
   } else if (sel && is_agent) {
-    dist_out = __fsqrt_rn(sqsum_1d(__fsub_rn(gx, px), __fsub_rn(gy, py), __fsub_rn(gz, pz)));
+    dist_out = sqrt_rn(sqsum_1d(__fsub_rn(gx, px), __fsub_rn(gy, py), __fsub_rn(gz, pz)));
   }
 
   // ---- observation row: [p | v | g-p | K x (p_j-p_i, d) | Ms x (o_m-p_i, d)]
@@ -462,7 +468,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     row[0] = px; row[1] = py; row[2] = pz;
     if constexpr (DYN == DYN_PHYS) {  // velocity clamped in the obs only (drone_physics_env.py:438-442)
       const double dvx = (double)vx, dvy = (double)vy, dvz = (double)vz;
-      const double nv = __dsqrt_rn(__dadd_rn(__dadd_rn(__dmul_rn(dvx, dvx), __dmul_rn(dvy, dvy)), __dmul_rn(dvz, dvz)));
+      const double nv = dsqrt_rn(__dadd_rn(__dadd_rn(__dmul_rn(dvx, dvx), __dmul_rn(dvy, dvy)), __dmul_rn(dvz, dvz)));
       if (nv > P.vmax_d) {
         row[3] = __double2float_rn(__dmul_rn(__ddiv_rn(dvx, nv), P.vmax_d));
         row[4] = __double2float_rn(__dmul_rn(__ddiv_rn(dvy, nv), P.vmax_d));
@@ -481,7 +487,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       uint64_t k2[KS];
 #pragma unroll
       for (int s = 0; s < KS; ++s)
-        k2[s] = (nk[s] == KEY_EMPTY) ? KEY_EMPTY : make_key(__fsqrt_rn(key_val(nk[s])), key_idx(nk[s]));
+        k2[s] = (nk[s] == KEY_EMPTY) ? KEY_EMPTY : make_key(sqrt_rn(key_val(nk[s])), key_idx(nk[s]));
 #pragma unroll
       for (int s = 1; s < KS; ++s) {
 #pragma unroll
