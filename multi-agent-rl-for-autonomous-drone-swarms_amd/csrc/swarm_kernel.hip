@@ -1,21 +1,22 @@
-// swarm_kernel.hip — fused swarm step / reset / observe kernel for gfx950 (MI355X, CDNA4),
+// swarm_kernel.hip — fused swarm step / reset / observe kernels for gfx950 (MI355X, CDNA4),
 // plus the C-ABI entry points declared in include/swarm_mi355x.h.
 //
-// One launch processes E envs.  A "team" of L = next_pow2(N) lanes owns one env (one lane per
-// drone); a 256-thread workgroup holds G = 256/L teams (N <= 256) or one team of L lanes.
-// Per launch and env:
-//   HBM -> regs/LDS : own pos/vel/action (12 B each per lane, coalesced), goal, obstacles
-//   integrate       : kinematic Euler (drone_swarm_env.py:103-117) or the point-mass
-//                     restatement of the PyBullet substep loop (drone_physics_env.py:323-360)
-//   pair pass       : every lane scans all N drones from LDS (broadcast reads): exact float
-//                     squared distance, top-(K+1) (s, j) keys, collision, formation sum
-//   obstacle pass   : exact axis-path distances, top-Ms keys, obstacle collision
-//   reductions      : team LDS counters (any_collision, continuing count)
-//   auto-reset      : Philox4x32-10 draws + a second kNN pass for envs whose episode ended
-//   obs             : rows staged in LDS [team][N][D] then stored as 16-B coalesced writes
+// A "team" of L = next_pow2(N) lanes owns one env (one lane per drone).
+//   WAVE kernel  (L <= 64): 64-thread workgroups = one wave holding G = 64/L teams.  The N x N
+//                pair pass is symmetric: at rotation r every lane computes the exact squared
+//                distance to drone t+r and receives the one drone t-r computed for it by
+//                ds_bpermute, so each unordered pair is evaluated once.  Team reductions are
+//                wave ballots; no cross-wave barrier exists.
+//   BLOCK kernel (L > 64): one env per workgroup of L threads; ascending broadcast pair loop
+//                from LDS; reductions with __syncthreads_count/or.
+// Both keep the top-(K+1) neighbours as packed 32-bit keys (float bits of the squared distance
+// with the low index bits replaced by the neighbour index) updated by one v_med3_u32 per slot;
+// the survivors are re-ranked by exact distance and an exactness test falls back to a full exact
+// selection in the rare near-tie case, so observations stay bit-exact.
+// Obs rows are staged through a small LDS chunk and stored as 16-B coalesced writes.
 //
-// Bit-exactness (SURVEY.md §8a parity spec): no FP contraction (-ffp-contract=off + explicit
-// __f*_rn / __d*_rn), correctly rounded sqrt/div where the reference's value is observable.
+// Bit-exactness: no FP contraction, IEEE sqrt/div where the reference's value is
+// observable, the sdot double-accumulated norm for 1-D norms and the float axis norm for obstacles.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -26,9 +27,11 @@
 
 #include "swarm_mi355x.h"
 
+#pragma clang fp contract(off)
+
 namespace {
 
-constexpr uint64_t KEY_EMPTY = ~0ull;
+constexpr uint32_t KEY_EMPTY = 0xffffffffu;
 constexpr int MODE_STEP = 0;
 constexpr int MODE_RESET = 1;
 constexpr int MODE_OBSERVE = 2;
@@ -37,58 +40,56 @@ constexpr int DYN_PHYS = SWARM_DYN_POINTMASS_PHYSICS;
 constexpr int MAX_N = 1024;
 constexpr int MAX_K = 16;
 constexpr int MAX_MS = 16;
-constexpr int STAGE_LDS_BUDGET = 64 * 1024;  // stage obs through LDS below this footprint
+constexpr int STAGE_BUDGET = 8 * 1024;  // bytes of LDS for one obs staging chunk
 constexpr int LDS_LIMIT = 160 * 1024;
+constexpr float PAD_POS = 1e18f;        // position of padding lanes (t >= N): never a neighbour
 
 // Derived, launch-ready parameters (host computes once per call).
 struct KParams {
-  int E, N, M, K, Ms, D, max_steps, reward_mode, auto_reset, substeps, damping_law;
-  int lanes, log2_lanes, envs_per_block, stage_obs, obs_vec4;
-  int pos_stride, obst_stride;  // float4 per team in LDS (padded by one to spread banks)
-  int off_obst, off_team, off_block, off_stage;
+  int E, N, M, K, Ms, D, max_steps, auto_reset, substeps, damping_law;
+  int lanes, log2_lanes, envs_per_block, threads, chunk_rows, obs_vec4;
+  int off_obst, off_stage, obst_stride;
+  uint32_t nb_keep, ob_keep;        // key masks: high bits kept from the distance, low bits = index
   long long env_offset;
   unsigned seed_lo, seed_hi;
   float half_w, neg_half_w, width_w;
-  float dt, vmax, amax, eps_speed;
+  float dt, vmax, amax, eps_speed, ds_f;
   float s_pair, s_obst;             // kinematic collision thresholds in squared-distance space
   float s_phys_pair, s_phys_obst, ground_z;
   float h, g, gcomp;
-  double goal_radius, desired_spacing, kp, r_goal, r_col, kf, vmax_d;
+  double goal_radius, kp, r_goal, r_col, kf, vmax_d;
 };
 
 // ------------------------------------------------------------------ exact numerics
-// No FP contraction anywhere in this file (the reference's NumPy ops round every product).
-#pragma clang fp contract(off)
 // Correctly rounded square roots.  NB: HIP's __fsqrt_rn is v_sqrt_f32 (1 ulp) unless
 // OCML_BASIC_ROUNDED_OPERATIONS is defined; llvm.sqrt lowers to the IEEE-exact sequence.
 __device__ __forceinline__ float sqrt_rn(float x) { return __builtin_sqrtf(x); }
 __device__ __forceinline__ double dsqrt_rn(double x) { return __builtin_sqrt(x); }
 // np.linalg.norm(v) of a float32 3-vector: OpenBLAS sdot = double accumulation of float
-// products, rounded to float; sqrt in float.  Returns the float sum s (d = sqrtf(s)).
+// products, rounded to float.  Returns the float sum s; the norm is sqrt_rn(s).
 __device__ __forceinline__ float sqsum_1d(float x, float y, float z) {
-  const float xx = __fmul_rn(x, x), yy = __fmul_rn(y, y), zz = __fmul_rn(z, z);
-  return __double2float_rn(__dadd_rn(__dadd_rn((double)xx, (double)yy), (double)zz));
+  const float xx = x * x, yy = y * y, zz = z * z;
+  return (float)(((double)xx + (double)yy) + (double)zz);
 }
 // np.linalg.norm(A, axis=1): float32 ((x*x)+(y*y))+(z*z).
 __device__ __forceinline__ float sqsum_axis(float x, float y, float z) {
-  return __fadd_rn(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y)), __fmul_rn(z, z));
+  return ((x * x) + (y * y)) + (z * z);
 }
-__device__ __forceinline__ uint64_t make_key(float v, int idx) {
-  return ((uint64_t)__float_as_uint(v) << 32) | (uint32_t)idx;
-}
-__device__ __forceinline__ float key_val(uint64_t k) { return __uint_as_float((uint32_t)(k >> 32)); }
-__device__ __forceinline__ int key_idx(uint64_t k) { return (int)(uint32_t)(k & 0xffffffffu); }
 
-// Insert `key` into the ascending list k[0..S-1], dropping the largest.
+__device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// Insert key into the ascending list k[0..S-1] (drops the largest): one med3 per slot.
 template <int S>
-__device__ __forceinline__ void topk_insert(uint64_t (&k)[S], uint64_t key) {
+__device__ __forceinline__ void kins(uint32_t (&k)[S], uint32_t key) {
 #pragma unroll
-  for (int s = S - 1; s > 0; --s) {
-    const uint64_t lo = k[s - 1];
-    const uint64_t cur = k[s];
-    k[s] = (key < lo) ? lo : ((key < cur) ? key : cur);
-  }
-  k[0] = (key < k[0]) ? key : k[0];
+  for (int s = S - 1; s > 0; --s) k[s] = med3u(k[s - 1], key, k[s]);
+  k[0] = min(k[0], key);
+}
+__device__ __forceinline__ uint32_t pack(float s, uint32_t keep, uint32_t idx) {
+  return (__float_as_uint(s) & keep) | idx;
 }
 
 // ------------------------------------------------------------------ Philox4x32-10 (device reset)
@@ -108,8 +109,8 @@ __device__ __forceinline__ void philox4x32_10(uint32_t (&c)[4], uint32_t k0, uin
   }
 }
 __device__ __forceinline__ float uni(uint32_t x, float lo, float width) {
-  const float u = __fmul_rn((float)(x >> 8), 0x1p-24f);
-  return __fadd_rn(lo, __fmul_rn(u, width));
+  const float u = (float)(x >> 8) * 0x1p-24f;
+  return lo + u * width;
 }
 __device__ __forceinline__ void draw_block(const KParams& P, long long genv, uint32_t episode,
                                            uint32_t block, uint32_t (&w)[4]) {
@@ -120,29 +121,64 @@ __device__ __forceinline__ void draw_block(const KParams& P, long long genv, uin
   philox4x32_10(w, P.seed_lo, P.seed_hi);
 }
 
-// ------------------------------------------------------------------ passes
-// PASS 0: kNN keys only.  PASS 1: kinematic step (+ collision among active drones, formation).
-// PASS 2: physics step (+ collision among all drones).
+// ------------------------------------------------------------------ pair passes
+// PASS 0: kNN keys only.  PASS 1: kinematic (+ collision and formation over active pairs).
+// PASS 2: physics (+ collision over all real drones).  `self` = this drone's flag (active in
+// kinematic mode, real drone in physics mode); pos4[j].w carries the same flag of drone j.
 template <int KS, int PASS>
-__device__ __forceinline__ void neighbor_pass(const float4* __restrict__ pos4, int N, int t,
-                                              float px, float py, float pz, bool act_i,
-                                              float s_thr, double ds, uint64_t (&nk)[KS > 0 ? KS : 1],
-                                              bool& coll, double& fsum) {
+__device__ __forceinline__ void pair_pass_wave(const float4* __restrict__ pos4, int L, int t, int lane0,
+                                               float px, float py, float pz, bool self, uint32_t keep,
+                                               float s_thr, float ds, uint32_t (&nk)[KS > 0 ? KS : 1],
+                                               bool& coll, double& fsum) {
+  const int half = L >> 1;
+  const uint32_t sflag = self ? 0u : 0x80000000u;
+#pragma unroll 2
+  for (int r = 1; r <= half; ++r) {
+    const int j = (t + r) & (L - 1);
+    const float4 q = pos4[j];
+    const float s = sqsum_1d(q.x - px, q.y - py, q.z - pz);
+    const uint32_t sb = __float_as_uint(s);
+    if constexpr (KS > 0) kins<KS>(nk, (sb & keep) | (uint32_t)j);
+    if constexpr (PASS == 1) {
+      const bool pr = self && (q.w != 0.f);
+      coll = coll || (pr && (s <= s_thr));
+      const float e = fabsf(__builtin_amdgcn_sqrtf(s) - ds);
+      fsum += (double)(pr ? e : 0.f);
+    } else if constexpr (PASS == 2) {
+      coll = coll || ((q.w != 0.f) && (s <= s_thr));
+    }
+    if (r < half) {  // mirror: drone m = t-r evaluated the pair (m, t) at this rotation
+      const int m = (t - r) & (L - 1);
+      const uint32_t recv = (uint32_t)__builtin_amdgcn_ds_bpermute((lane0 + m) << 2, (int)(sb | sflag));
+      const uint32_t rb = recv & 0x7fffffffu;
+      if constexpr (KS > 0) kins<KS>(nk, (rb & keep) | (uint32_t)m);
+      if constexpr (PASS == 1) {
+        const bool pr = self && !(recv >> 31);
+        const float sm = __uint_as_float(rb);
+        coll = coll || (pr && (sm <= s_thr));
+        const float e = fabsf(__builtin_amdgcn_sqrtf(sm) - ds);
+        fsum += (double)(pr ? e : 0.f);
+      } else if constexpr (PASS == 2) {
+        coll = coll || (!(recv >> 31) && (__uint_as_float(rb) <= s_thr));
+      }
+    }
+  }
+}
+
+template <int KS, int PASS>
+__device__ __forceinline__ void pair_pass_block(const float4* __restrict__ pos4, int N, int t, float px, float py,
+                                                float pz, bool self, uint32_t keep, float s_thr, float ds,
+                                                uint32_t (&nk)[KS > 0 ? KS : 1], bool& coll, double& fsum) {
+#pragma unroll 4
   for (int j = 0; j < N; ++j) {
     const float4 q = pos4[j];
-    const float s = sqsum_1d(__fsub_rn(q.x, px), __fsub_rn(q.y, py), __fsub_rn(q.z, pz));
-    if constexpr (KS > 0) {
-      const uint64_t key = (j == t) ? KEY_EMPTY : make_key(s, j);
-      topk_insert<KS>(nk, key);
-    }
+    const float s = sqsum_1d(q.x - px, q.y - py, q.z - pz);
+    if constexpr (KS > 0) kins<KS>(nk, (j == t) ? KEY_EMPTY : pack(s, keep, (uint32_t)j));
     if constexpr (PASS == 1) {
-      const bool pair = act_i && (q.w != 0.0f) && (j != t);
-      coll = coll || (pair && (s <= s_thr));
-      // formation uses d_ij widened to double; v_sqrt_f32 (<=1 ulp) keeps the reward within
-      // ~1e-7 of the reference's mean, well inside the 1e-5 contract.
-      const float d = __builtin_amdgcn_sqrtf(s);
-      const double e = fabs(__dsub_rn((double)d, ds));
-      fsum = __dadd_rn(fsum, pair ? e : 0.0);
+      const bool pr = self && (q.w != 0.f) && (j != t);
+      coll = coll || (pr && (s <= s_thr));
+      const float e = fabsf(__builtin_amdgcn_sqrtf(s) - ds);
+      fsum += (double)(pr ? e : 0.f);
     } else if constexpr (PASS == 2) {
       coll = coll || ((j != t) && (s <= s_thr));
     }
@@ -150,20 +186,87 @@ __device__ __forceinline__ void neighbor_pass(const float4* __restrict__ pos4, i
 }
 
 template <int MSL, bool COLL>
-__device__ __forceinline__ void obstacle_pass(const float4* __restrict__ obst4, int M, float px,
-                                              float py, float pz, bool chk, float s_thr,
-                                              uint64_t (&ok)[MSL > 0 ? MSL : 1], bool& coll) {
+__device__ __forceinline__ void obstacle_pass(const float4* __restrict__ obst4, int M, float px, float py, float pz,
+                                              bool chk, float s_thr, uint32_t keep,
+                                              uint32_t (&ok)[MSL > 0 ? MSL : 1], bool& coll) {
   for (int m = 0; m < M; ++m) {
     const float4 q = obst4[m];
-    const float s = sqsum_axis(__fsub_rn(q.x, px), __fsub_rn(q.y, py), __fsub_rn(q.z, pz));
-    if constexpr (MSL > 0) topk_insert<MSL>(ok, make_key(sqrt_rn(s), m));
+    const float s = sqsum_axis(q.x - px, q.y - py, q.z - pz);
+    if constexpr (MSL > 0) kins<MSL>(ok, pack(s, keep, (uint32_t)m));
     if constexpr (COLL) coll = coll || (chk && (s <= s_thr));
   }
 }
 
+// Re-rank the S surviving keys by exact distance (the reference sorts by the float distance;
+// ties by index).  Returns false when an entry outside the survivors could still precede the
+// K-th winner (near-tie at truncation granularity) — the caller then runs exact_select.
+template <int S, bool AXIS>
+__device__ __forceinline__ bool finish_keys(const uint32_t (&k)[S], const float4* __restrict__ pts, int count, int K,
+                                            uint32_t keep, float px, float py, float pz, float (&wd)[S],
+                                            int (&wj)[S]) {
+  const uint32_t imask = ~keep;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const uint32_t key = k[s];
+    const int j = (int)(key & imask);
+    const bool valid = (key != KEY_EMPTY) && (j < count);
+    float d = __builtin_inff();
+    if (valid) {
+      const float4 q = pts[j];
+      d = AXIS ? sqrt_rn(sqsum_axis(q.x - px, q.y - py, q.z - pz)) : sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
+    }
+    wd[s] = d;
+    wj[s] = valid ? j : 0x7fffffff;
+  }
+#pragma unroll
+  for (int s = 1; s < S; ++s) {
+#pragma unroll
+    for (int r = s; r > 0; --r) {
+      const float a = wd[r - 1], b = wd[r];
+      const int ja = wj[r - 1], jb = wj[r];
+      const bool sw = (b < a) || (b == a && jb < ja);
+      wd[r - 1] = sw ? b : a; wd[r] = sw ? a : b;
+      wj[r - 1] = sw ? jb : ja; wj[r] = sw ? ja : jb;
+    }
+  }
+  const uint32_t last = k[S - 1];
+  if (last == KEY_EMPTY || (int)(last & imask) >= count) return true;
+  if (K <= 0) return true;
+  const float dlb = sqrt_rn(__uint_as_float(last & keep));
+  return dlb > wd[K - 1];
+}
+
+// Exact (distance, index) selection of the K nearest of `count` points (rare fallback).
+template <int S, bool AXIS>
+__device__ __forceinline__ void exact_select(const float4* __restrict__ pts, int count, int self, int K, float px,
+                                          float py, float pz, float (&wd)[S], int (&wj)[S]) {
+  float pd = -1.f;
+  int pj = -1;
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    float bd = __builtin_inff();
+    int bj = 0x7fffffff;
+    if (k < K) {
+      for (int j = 0; j < count; ++j) {
+        if (j == self) continue;
+        const float4 q = pts[j];
+        const float d = AXIS ? sqrt_rn(sqsum_axis(q.x - px, q.y - py, q.z - pz))
+                             : sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
+        const bool gt = (d > pd) || (d == pd && j > pj);
+        const bool lt = (d < bd) || (d == bd && j < bj);
+        if (gt && lt) { bd = d; bj = j; }
+      }
+    }
+    wd[k] = bd;
+    wj[k] = bj;
+    pd = bd;
+    pj = bj;
+  }
+}
+
 // ------------------------------------------------------------------ the kernel
-template <int DYN, int KS, int MSL>
-__global__ void __launch_bounds__(1024)
+template <int DYN, int KS, int MSL, bool WAVE>
+__global__ void __launch_bounds__(WAVE ? 64 : 1024)
 swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ actions,
              const uint8_t* __restrict__ amask, const swarm_out_t O,
              const uint8_t* __restrict__ env_mask, int mode) {
@@ -173,24 +276,23 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   const int team = tid >> P.log2_lanes;
   const int t = tid & (L - 1);
   const int G = P.envs_per_block;
-  const int N = P.N, M = P.M, D = P.D;
+  const int N = P.N, M = P.M, D = P.D, K = P.K, Ms = P.Ms;
   const long long env0 = (long long)blockIdx.x * G;
   const long long env = env0 + team;
   const bool env_ok = env < P.E;
   const bool is_agent = env_ok && t < N;
-  float4* pos4 = reinterpret_cast<float4*>(smem) + team * P.pos_stride;
+  const int lane0 = team * L;  // first thread of this team
+  float4* pos4 = reinterpret_cast<float4*>(smem) + lane0;
   float4* obst4 = reinterpret_cast<float4*>(smem + P.off_obst) + team * P.obst_stride;
-  int* tint = reinterpret_cast<int*>(smem + P.off_team) + team * 4;
-  int* bflag = reinterpret_cast<int*>(smem + P.off_block);
   float* stage = reinterpret_cast<float*>(smem + P.off_stage);
+  uint64_t team_bits = 0;
+  if constexpr (WAVE) team_bits = (L == 64) ? ~0ull : (((1ull << L) - 1ull) << lane0);
 
   // envs this call writes: every env (step) or the masked ones (reset / observe)
   bool sel = env_ok;
   if (mode != MODE_STEP && env_mask != nullptr && env_ok) sel = env_mask[env] != 0;
 
   // ---- load
-  if (t == 0) { tint[0] = 0; tint[1] = 0; tint[2] = 0; tint[3] = 0; }
-  if (tid == 0) bflag[0] = 0;
   int stepc = 0;
   float gx = 0.f, gy = 0.f, gz = 0.f;
   if (env_ok) {
@@ -203,7 +305,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     gz = S.goal[env * 3 + 2];
     stepc = S.step_count[env];
   }
-  float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f, damp = 0.f;
+  float px = PAD_POS, py = PAD_POS, pz = PAD_POS, vx = 0.f, vy = 0.f, vz = 0.f, damp = 0.f;
   bool act = false;
   const long long ag = env * N + t;
   if (is_agent) {
@@ -212,10 +314,9 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     act = S.active[ag] != 0;
     if constexpr (DYN == DYN_PHYS) damp = S.damping[ag];
   }
-  __syncthreads();
-  if (is_agent && act) atomicAdd(&tint[0], 1);
-  __syncthreads();
-  const int n_active = tint[0];
+  int n_active;
+  if constexpr (WAVE) n_active = __popcll(__ballot(is_agent && act) & team_bits);
+  else n_active = __syncthreads_count(is_agent && act);
 
   // ---- integrate (step) or draw (explicit reset)
   float prev_d = 0.f;
@@ -226,23 +327,23 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     const bool has = (amask == nullptr) || (amask[ag] != 0);
     if constexpr (DYN == DYN_KIN) {
       if (act) {  // drone_swarm_env.py:98-111
-        prev_d = sqrt_rn(sqsum_1d(__fsub_rn(gx, px), __fsub_rn(gy, py), __fsub_rn(gz, pz)));
+        prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
         if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
-        ax = __fmul_rn(fminf(fmaxf(ax, -1.f), 1.f), P.amax);
-        ay = __fmul_rn(fminf(fmaxf(ay, -1.f), 1.f), P.amax);
-        az = __fmul_rn(fminf(fmaxf(az, -1.f), 1.f), P.amax);
-        vx = __fadd_rn(vx, __fmul_rn(ax, P.dt));
-        vy = __fadd_rn(vy, __fmul_rn(ay, P.dt));
-        vz = __fadd_rn(vz, __fmul_rn(az, P.dt));
+        ax = fminf(fmaxf(ax, -1.f), 1.f) * P.amax;
+        ay = fminf(fmaxf(ay, -1.f), 1.f) * P.amax;
+        az = fminf(fmaxf(az, -1.f), 1.f) * P.amax;
+        vx = vx + ax * P.dt;
+        vy = vy + ay * P.dt;
+        vz = vz + az * P.dt;
         const float sp = sqrt_rn(sqsum_1d(vx, vy, vz));  // _clip_speed :179-183
         if (!(sp <= P.vmax || sp < P.eps_speed)) {
-          vx = __fmul_rn(__fdiv_rn(vx, sp), P.vmax);
-          vy = __fmul_rn(__fdiv_rn(vy, sp), P.vmax);
-          vz = __fmul_rn(__fdiv_rn(vz, sp), P.vmax);
+          vx = (vx / sp) * P.vmax;
+          vy = (vy / sp) * P.vmax;
+          vz = (vz / sp) * P.vmax;
         }
-        px = __fadd_rn(px, __fmul_rn(vx, P.dt));
-        py = __fadd_rn(py, __fmul_rn(vy, P.dt));
-        pz = __fadd_rn(pz, __fmul_rn(vz, P.dt));
+        px = px + vx * P.dt;
+        py = py + vy * P.dt;
+        pz = pz + vz * P.dt;
       }
       if (n_active > 0) {  // world clip of ALL drones, :113-117
         px = fminf(fmaxf(px, P.neg_half_w), P.half_w);
@@ -252,33 +353,33 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     } else {
       // point-mass restatement of drone_physics_env.py:323-360
       const float h = P.h;
-      const float cx = has ? __fmul_rn(ax, P.amax) : 0.f;
-      const float cy = has ? __fmul_rn(ay, P.amax) : 0.f;
-      float cz = has ? __fadd_rn(__fmul_rn(az, P.amax), P.gcomp) : 0.f;
-      cz = __fadd_rn(cz, P.g);
+      const float cx = has ? ax * P.amax : 0.f;
+      const float cy = has ? ay * P.amax : 0.f;
+      float cz = has ? az * P.amax + P.gcomp : 0.f;
+      cz = cz + P.g;
       float fac = 1.f;
-      if (P.damping_law == 1) fac = __double2float_rn(pow((double)__fsub_rn(1.f, damp), (double)h));
+      if (P.damping_law == 1) fac = (float)pow((double)(1.f - damp), (double)h);
       for (int s = 0; s < P.substeps; ++s) {
         const float sp = sqrt_rn(sqsum_1d(vx, vy, vz));
         if (has && sp > P.vmax) {
-          vx = __fmul_rn(__fdiv_rn(vx, sp), P.vmax);
-          vy = __fmul_rn(__fdiv_rn(vy, sp), P.vmax);
-          vz = __fmul_rn(__fdiv_rn(vz, sp), P.vmax);
+          vx = (vx / sp) * P.vmax;
+          vy = (vy / sp) * P.vmax;
+          vz = (vz / sp) * P.vmax;
         }
         if (P.damping_law == 0) {
           const float sp2 = sqrt_rn(sqsum_1d(vx, vy, vz));
-          const float c = __fmul_rn(damp, __fadd_rn(1.f, sp2));
-          vx = __fadd_rn(vx, __fmul_rn(h, __fsub_rn(cx, __fmul_rn(c, vx))));
-          vy = __fadd_rn(vy, __fmul_rn(h, __fsub_rn(cy, __fmul_rn(c, vy))));
-          vz = __fadd_rn(vz, __fmul_rn(h, __fsub_rn(cz, __fmul_rn(c, vz))));
+          const float c = damp * (1.f + sp2);
+          vx = vx + h * (cx - c * vx);
+          vy = vy + h * (cy - c * vy);
+          vz = vz + h * (cz - c * vz);
         } else {
-          vx = __fmul_rn(__fadd_rn(vx, __fmul_rn(h, cx)), fac);
-          vy = __fmul_rn(__fadd_rn(vy, __fmul_rn(h, cy)), fac);
-          vz = __fmul_rn(__fadd_rn(vz, __fmul_rn(h, cz)), fac);
+          vx = (vx + h * cx) * fac;
+          vy = (vy + h * cy) * fac;
+          vz = (vz + h * cz) * fac;
         }
-        px = __fadd_rn(px, __fmul_rn(h, vx));
-        py = __fadd_rn(py, __fmul_rn(h, vy));
-        pz = __fadd_rn(pz, __fmul_rn(h, vz));
+        px = px + h * vx;
+        py = py + h * vy;
+        pz = pz + h * vz;
       }
     }
   }
@@ -296,7 +397,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       act = true;
       if constexpr (DYN == DYN_PHYS) {
         pz = fmaxf(pz, 1.0f);
-        damp = __fmul_rn(0.5f, uni(w[3], 0.8f, 0.4f));
+        damp = 0.5f * uni(w[3], 0.8f, 0.4f);
       }
     }
     for (int m = t; m < M; m += L) {
@@ -313,34 +414,37 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     stepc = 0;
   }
 
-  if (is_agent) {
-    const float wflag = (DYN == DYN_KIN) ? (act ? 1.f : 0.f) : 1.f;
-    pos4[t] = make_float4(px, py, pz, wflag);
-  }
+  // LDS slot: (p, flag); padding lanes sit far away with flag 0
+  const float wflag = (DYN == DYN_KIN) ? (act ? 1.f : 0.f) : (is_agent ? 1.f : 0.f);
+  pos4[t] = make_float4(px, py, pz, wflag);
   __syncthreads();
 
   // ---- pair + obstacle passes
-  uint64_t nk[KS > 0 ? KS : 1];
-  uint64_t ok[MSL > 0 ? MSL : 1];
+  uint32_t nk[KS > 0 ? KS : 1];
+  uint32_t ok[MSL > 0 ? MSL : 1];
 #pragma unroll
   for (int s = 0; s < (KS > 0 ? KS : 1); ++s) nk[s] = KEY_EMPTY;
 #pragma unroll
   for (int s = 0; s < (MSL > 0 ? MSL : 1); ++s) ok[s] = KEY_EMPTY;
   bool coll = false;
   double fsum = 0.0;
-  const bool do_pass = is_agent && (mode == MODE_STEP || sel);
-  if (do_pass) {
+  const bool pass_env = (mode == MODE_STEP) ? env_ok : sel;
+  const bool self_flag = (DYN == DYN_KIN) ? act : is_agent;
+  if (pass_env) {
     if (mode == MODE_STEP) {
       if constexpr (DYN == DYN_KIN) {
-        neighbor_pass<KS, 1>(pos4, N, t, px, py, pz, act, P.s_pair, P.desired_spacing, nk, coll, fsum);
-        obstacle_pass<MSL, true>(obst4, M, px, py, pz, act, P.s_obst, ok, coll);
+        if constexpr (WAVE) pair_pass_wave<KS, 1>(pos4, L, t, lane0, px, py, pz, self_flag, P.nb_keep, P.s_pair, P.ds_f, nk, coll, fsum);
+        else pair_pass_block<KS, 1>(pos4, N, t, px, py, pz, self_flag, P.nb_keep, P.s_pair, P.ds_f, nk, coll, fsum);
+        obstacle_pass<MSL, true>(obst4, M, px, py, pz, act, P.s_obst, P.ob_keep, ok, coll);
       } else {
-        neighbor_pass<KS, 2>(pos4, N, t, px, py, pz, act, P.s_phys_pair, 0.0, nk, coll, fsum);
-        obstacle_pass<MSL, true>(obst4, M, px, py, pz, true, P.s_phys_obst, ok, coll);
+        if constexpr (WAVE) pair_pass_wave<KS, 2>(pos4, L, t, lane0, px, py, pz, self_flag, P.nb_keep, P.s_phys_pair, 0.f, nk, coll, fsum);
+        else pair_pass_block<KS, 2>(pos4, N, t, px, py, pz, self_flag, P.nb_keep, P.s_phys_pair, 0.f, nk, coll, fsum);
+        obstacle_pass<MSL, true>(obst4, M, px, py, pz, true, P.s_phys_obst, P.ob_keep, ok, coll);
       }
     } else {
-      neighbor_pass<KS, 0>(pos4, N, t, px, py, pz, act, 0.f, 0.0, nk, coll, fsum);
-      obstacle_pass<MSL, false>(obst4, M, px, py, pz, false, 0.f, ok, coll);
+      if constexpr (WAVE) pair_pass_wave<KS, 0>(pos4, L, t, lane0, px, py, pz, self_flag, P.nb_keep, 0.f, 0.f, nk, coll, fsum);
+      else pair_pass_block<KS, 0>(pos4, N, t, px, py, pz, self_flag, P.nb_keep, 0.f, 0.f, nk, coll, fsum);
+      obstacle_pass<MSL, false>(obst4, M, px, py, pz, false, 0.f, P.ob_keep, ok, coll);
     }
   }
 
@@ -349,50 +453,58 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   bool term = false, trunc = false, cont = false, reached = false, collided = false;
   bool term_all = false, trunc_all = false, do_reset = false;
   int new_step = stepc;
-  double dist_phys = 0.0;
   if (mode == MODE_STEP) {
+    bool p_coll = false, p_cand = false, p_notall = false;
     if (is_agent) {
       if constexpr (DYN == DYN_KIN) {
-        const float curr = sqrt_rn(sqsum_1d(__fsub_rn(gx, px), __fsub_rn(gy, py), __fsub_rn(gz, pz)));
+        const float curr = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
         dist_out = curr;
         if (act) {
           reached = (double)curr <= P.goal_radius;  // fp64 compare, :124-127
           collided = coll;
-          if (collided) atomicOr(&tint[1], 1);
-          if (!reached && !collided) atomicAdd(&tint[2], 1);
-          double r = __dmul_rn(__dsub_rn((double)prev_d, (double)curr), P.kp);
-          if (n_active > 1) r = __dadd_rn(r, __dmul_rn(-P.kf, __ddiv_rn(fsum, (double)(n_active - 1))));
-          if (reached) r = __dadd_rn(r, P.r_goal);
-          if (collided) r = __dadd_rn(r, P.r_col);
-          rew = __double2float_rn(r);
+          p_coll = collided;
+          p_cand = !reached && !collided;
+          double r = ((double)prev_d - (double)curr) * P.kp;
+          if (n_active > 1) r = r + (-P.kf) * (fsum / (double)(n_active - 1));
+          if (reached) r = r + P.r_goal;
+          if (collided) r = r + P.r_col;
+          rew = (float)r;
         }
       } else {
-        const double dx = __dsub_rn((double)px, (double)gx);
-        const double dy = __dsub_rn((double)py, (double)gy);
-        const double dz = __dsub_rn((double)pz, (double)gz);
-        dist_phys = dsqrt_rn(__dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)));
-        dist_out = __double2float_rn(dist_phys);
+        const double dx = (double)px - (double)gx;
+        const double dy = (double)py - (double)gy;
+        const double dz = (double)pz - (double)gz;
+        const double dist_phys = dsqrt_rn(((dx * dx) + (dy * dy)) + (dz * dz));
+        dist_out = (float)dist_phys;
         collided = coll || (pz <= P.ground_z);
         reached = dist_phys < P.goal_radius;
         if (act) {
-          if (collided) atomicOr(&tint[1], 1);
-          if (!collided && !reached) atomicOr(&tint[3], 1);
-          double r = __dmul_rn(-dist_phys, 0.1);
-          if (collided) r = __dsub_rn(r, 10.0);
-          else if (reached) r = __dadd_rn(r, 50.0);
-          rew = __double2float_rn(r);
+          p_coll = collided;
+          p_notall = !collided && !reached;
+          double r = (-dist_phys) * 0.1;
+          if (collided) r = r - 10.0;
+          else if (reached) r = r + 50.0;
+          rew = (float)r;
         }
       }
     }
-    __syncthreads();
-    const bool any_c = tint[1] != 0;
+    bool any_c, any_cand, any_notall;
+    if constexpr (WAVE) {
+      any_c = (__ballot(p_coll) & team_bits) != 0;
+      any_cand = (__ballot(p_cand) & team_bits) != 0;
+      any_notall = (__ballot(p_notall) & team_bits) != 0;
+    } else {
+      any_c = __syncthreads_or(p_coll) != 0;
+      any_cand = __syncthreads_or(p_cand) != 0;
+      any_notall = __syncthreads_or(p_notall) != 0;
+    }
     if constexpr (DYN == DYN_KIN) {
       if (n_active == 0) {  // drone_swarm_env.py:93-95
         term_all = true;
       } else {
         new_step = stepc + 1;
         const bool tl = new_step >= P.max_steps;
-        const bool all_reached = (tint[2] == 0) && !any_c && !tl;
+        const bool all_reached = !any_cand && !any_c && !tl;
         term_all = all_reached || any_c;
         trunc_all = tl && !term_all;
         if (act) {
@@ -405,7 +517,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     } else {
       new_step = stepc + 1;
       const bool tl = new_step >= P.max_steps;
-      const bool all_goals = tint[3] == 0;
+      const bool all_goals = !any_notall;
       const bool done = any_c || all_goals || tl;
       trunc_all = done && tl && !any_c && !all_goals;
       term_all = done && !trunc_all;
@@ -414,22 +526,23 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       cont = true;
     }
     do_reset = P.auto_reset && env_ok && (term_all || trunc_all);
-    if (t == 0 && do_reset) atomicOr(bflag, 1);
-    __syncthreads();
-    if (bflag[0]) {  // block-uniform: some team re-draws its env in-kernel
+    bool any_reset;
+    if constexpr (WAVE) any_reset = __ballot(do_reset) != 0;
+    else any_reset = __syncthreads_or(do_reset) != 0;
+    if (any_reset) {  // block-uniform: some team re-draws its env in-kernel
+      __syncthreads();  // pass-1 reads of pos4/obst4 are done
       if (do_reset) {
         episode_new = S.episode[env] + 1u;
         uint32_t w[4];
         if (t < N) {
           draw_block(P, genv, episode_new, (uint32_t)t, w);
-          float nx = uni(w[0], P.neg_half_w, P.width_w);
-          float ny = uni(w[1], P.neg_half_w, P.width_w);
-          float nz = uni(w[2], P.neg_half_w, P.width_w);
+          px = uni(w[0], P.neg_half_w, P.width_w);
+          py = uni(w[1], P.neg_half_w, P.width_w);
+          pz = uni(w[2], P.neg_half_w, P.width_w);
           if constexpr (DYN == DYN_PHYS) {
-            nz = fmaxf(nz, 1.0f);
-            damp = __fmul_rn(0.5f, uni(w[3], 0.8f, 0.4f));
+            pz = fmaxf(pz, 1.0f);
+            damp = 0.5f * uni(w[3], 0.8f, 0.4f);
           }
-          px = nx; py = ny; pz = nz;
           vx = vy = vz = 0.f;
           pos4[t] = make_float4(px, py, pz, 1.f);
         }
@@ -446,115 +559,125 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         if constexpr (DYN == DYN_PHYS) gz = uni(w[3], 0.5f, 1.5f);
       }
       __syncthreads();
-      if (do_reset && is_agent) {
+      if (do_reset) {
 #pragma unroll
         for (int s = 0; s < (KS > 0 ? KS : 1); ++s) nk[s] = KEY_EMPTY;
 #pragma unroll
         for (int s = 0; s < (MSL > 0 ? MSL : 1); ++s) ok[s] = KEY_EMPTY;
         bool c2 = false;
         double f2 = 0.0;
-        neighbor_pass<KS, 0>(pos4, N, t, px, py, pz, true, 0.f, 0.0, nk, c2, f2);
-        obstacle_pass<MSL, false>(obst4, M, px, py, pz, false, 0.f, ok, c2);
+        const bool fl = t < N;
+        if constexpr (WAVE) pair_pass_wave<KS, 0>(pos4, L, t, lane0, px, py, pz, fl, P.nb_keep, 0.f, 0.f, nk, c2, f2);
+        else pair_pass_block<KS, 0>(pos4, N, t, px, py, pz, fl, P.nb_keep, 0.f, 0.f, nk, c2, f2);
+        obstacle_pass<MSL, false>(obst4, M, px, py, pz, false, 0.f, P.ob_keep, ok, c2);
       }
     }
   } else if (sel && is_agent) {
-    dist_out = sqrt_rn(sqsum_1d(__fsub_rn(gx, px), __fsub_rn(gy, py), __fsub_rn(gz, pz)));
+    dist_out = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
   }
 
-  // ---- observation row: [p | v | g-p | K x (p_j-p_i, d) | Ms x (o_m-p_i, d)]
+  // ---- exact neighbour / obstacle selection for the observation
   const bool write_env = (mode == MODE_STEP) ? env_ok : sel;
+  constexpr int NW = KS > 0 ? KS : 1;
+  constexpr int OW = MSL > 0 ? MSL : 1;
+  float wd[NW], od[OW];
+  int wj[NW], oj[OW];
+#pragma unroll
+  for (int s = 0; s < NW; ++s) { wd[s] = 0.f; wj[s] = 0x7fffffff; }
+#pragma unroll
+  for (int s = 0; s < OW; ++s) { od[s] = 0.f; oj[s] = 0x7fffffff; }
+  bool slow_nb = false, slow_ob = false;
   if (is_agent && write_env) {
-    float* row = P.stage_obs ? stage + (size_t)(team * N + t) * D : O.obs + (size_t)ag * D;
-    row[0] = px; row[1] = py; row[2] = pz;
-    if constexpr (DYN == DYN_PHYS) {  // velocity clamped in the obs only (drone_physics_env.py:438-442)
-      const double dvx = (double)vx, dvy = (double)vy, dvz = (double)vz;
-      const double nv = dsqrt_rn(__dadd_rn(__dadd_rn(__dmul_rn(dvx, dvx), __dmul_rn(dvy, dvy)), __dmul_rn(dvz, dvz)));
-      if (nv > P.vmax_d) {
-        row[3] = __double2float_rn(__dmul_rn(__ddiv_rn(dvx, nv), P.vmax_d));
-        row[4] = __double2float_rn(__dmul_rn(__ddiv_rn(dvy, nv), P.vmax_d));
-        row[5] = __double2float_rn(__dmul_rn(__ddiv_rn(dvz, nv), P.vmax_d));
-      } else {
-        row[3] = vx; row[4] = vy; row[5] = vz;
-      }
-    } else {
-      row[3] = vx; row[4] = vy; row[5] = vz;
-    }
-    row[6] = __fsub_rn(gx, px); row[7] = __fsub_rn(gy, py); row[8] = __fsub_rn(gz, pz);
-    int col = 9;
-    if constexpr (KS > 0) {
-      // keys were ranked by the exact float squared sum; re-rank the K+1 survivors by the exact
-      // distance so (d, j) order matches the reference's argsort on d
-      uint64_t k2[KS];
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-        k2[s] = (nk[s] == KEY_EMPTY) ? KEY_EMPTY : make_key(sqrt_rn(key_val(nk[s])), key_idx(nk[s]));
-#pragma unroll
-      for (int s = 1; s < KS; ++s) {
-#pragma unroll
-        for (int r = s; r > 0; --r) {
-          const uint64_t a = k2[r - 1], b = k2[r];
-          const bool sw = b < a;
-          k2[r - 1] = sw ? b : a;
-          k2[r] = sw ? a : b;
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < KS - 1; ++s) {
-        if (s < P.K) {
-          float f0 = 0.f, f1 = 0.f, f2 = 0.f, f3 = 0.f;
-          if (k2[s] != KEY_EMPTY) {
-            const float4 q = pos4[key_idx(k2[s])];
-            f0 = __fsub_rn(q.x, px); f1 = __fsub_rn(q.y, py); f2 = __fsub_rn(q.z, pz);
-            f3 = key_val(k2[s]);
-          }
-          row[col + 4 * s + 0] = f0; row[col + 4 * s + 1] = f1;
-          row[col + 4 * s + 2] = f2; row[col + 4 * s + 3] = f3;
-        }
-      }
-    }
-    col += 4 * P.K;  // neighbor_slots() guarantees KS >= K + 1
-    if (P.Ms > 0) {
-#pragma unroll
-      for (int s = 0; s < (MSL > 0 ? MSL : 1); ++s) {
-        if (s < P.Ms) {
-          float f0 = 0.f, f1 = 0.f, f2 = 0.f, f3 = 0.f;
-          if (MSL > 0 && ok[s] != KEY_EMPTY) {
-            const float4 q = obst4[key_idx(ok[s])];
-            f0 = __fsub_rn(q.x, px); f1 = __fsub_rn(q.y, py); f2 = __fsub_rn(q.z, pz);
-            f3 = key_val(ok[s]);
-          }
-          row[col + 4 * s + 0] = f0; row[col + 4 * s + 1] = f1;
-          row[col + 4 * s + 2] = f2; row[col + 4 * s + 3] = f3;
-        }
-      }
-      for (int s = (MSL > 0 ? MSL : 1); s < P.Ms; ++s) {  // Ms > slots only when Ms > M: padding
-        row[col + 4 * s + 0] = 0.f; row[col + 4 * s + 1] = 0.f;
-        row[col + 4 * s + 2] = 0.f; row[col + 4 * s + 3] = 0.f;
-      }
+    if constexpr (KS > 0) slow_nb = !finish_keys<KS, false>(nk, pos4, N, K, P.nb_keep, px, py, pz, wd, wj);
+    if constexpr (MSL > 0) slow_ob = !finish_keys<MSL, true>(ok, obst4, M, Ms < M ? Ms : M, P.ob_keep, px, py, pz, od, oj);
+  }
+  if constexpr (KS > 0) {
+    if (slow_nb) exact_select<NW, false>(pos4, N, t, K, px, py, pz, wd, wj);
+  }
+  if constexpr (MSL > 0) {
+    if (slow_ob) exact_select<OW, true>(obst4, M, -1, Ms < M ? Ms : M, px, py, pz, od, oj);
+  }
+
+  // observation velocity (physics clamps it in the obs only, drone_physics_env.py:438-442)
+  float ovx = vx, ovy = vy, ovz = vz;
+  if constexpr (DYN == DYN_PHYS) {
+    const double dvx = (double)vx, dvy = (double)vy, dvz = (double)vz;
+    const double nv = dsqrt_rn(((dvx * dvx) + (dvy * dvy)) + (dvz * dvz));
+    if (nv > P.vmax_d) {
+      ovx = (float)((dvx / nv) * P.vmax_d);
+      ovy = (float)((dvy / nv) * P.vmax_d);
+      ovz = (float)((dvz / nv) * P.vmax_d);
     }
   }
-  if (P.stage_obs) {
-    __syncthreads();
-    const int teamf = N * D;
-    if (mode == MODE_STEP || env_mask == nullptr) {
-      // whole block region [env0, env0+nvalid) is one contiguous run of floats
-      long long nvalid = P.E - env0;
-      if (nvalid > G) nvalid = G;
-      const long long total = nvalid * teamf;
-      float* dst = O.obs + env0 * teamf;
-      if (P.obs_vec4) {
-        const long long n4 = total >> 2;
-        const float4* s4 = reinterpret_cast<const float4*>(stage);
-        float4* d4 = reinterpret_cast<float4*>(dst);
-        for (long long i = tid; i < n4; i += blockDim.x) d4[i] = s4[i];
-        for (long long i = (n4 << 2) + tid; i < total; i += blockDim.x) dst[i] = stage[i];
-      } else {
-        for (long long i = tid; i < total; i += blockDim.x) dst[i] = stage[i];
+
+  // ---- observation rows: [p | v | g-p | K x (p_j-p_i, d) | Ms x (o_m-p_i, d)]
+  auto write_row = [&](float* row) {
+    row[0] = px; row[1] = py; row[2] = pz;
+    row[3] = ovx; row[4] = ovy; row[5] = ovz;
+    row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
+    int col = 9;
+    if constexpr (KS > 0) {
+#pragma unroll
+      for (int s = 0; s < KS - 1; ++s) {
+        if (s < K) {
+          float f0 = 0.f, f1 = 0.f, f2 = 0.f, f3 = 0.f;
+          if (wj[s] < N) {
+            const float4 q = pos4[wj[s]];
+            f0 = q.x - px; f1 = q.y - py; f2 = q.z - pz; f3 = wd[s];
+          }
+          row[col + 4 * s + 0] = f0; row[col + 4 * s + 1] = f1;
+          row[col + 4 * s + 2] = f2; row[col + 4 * s + 3] = f3;
+        }
       }
-    } else if (sel) {
-      const float* src = stage + (size_t)team * teamf;
-      float* dst = O.obs + env * teamf;
-      for (int i = t; i < teamf; i += L) dst[i] = src[i];
+    }
+    col += 4 * K;
+    for (int s = 0; s < Ms; ++s) {
+      float f0 = 0.f, f1 = 0.f, f2 = 0.f, f3 = 0.f;
+      int m = 0x7fffffff;
+      float d = 0.f;
+      if constexpr (MSL > 0) {
+#pragma unroll
+        for (int u = 0; u < MSL - 1; ++u)
+          if (u == s) { m = oj[u]; d = od[u]; }
+      }
+      if (m < M) {
+        const float4 q = obst4[m];
+        f0 = q.x - px; f1 = q.y - py; f2 = q.z - pz; f3 = d;
+      }
+      row[col + 4 * s + 0] = f0; row[col + 4 * s + 1] = f1;
+      row[col + 4 * s + 2] = f2; row[col + 4 * s + 3] = f3;
+    }
+  };
+
+  if (mode != MODE_STEP && env_mask != nullptr) {
+    // masked reset/observe: rows straight to global memory (off the hot path)
+    if (is_agent && sel) write_row(O.obs + (size_t)ag * D);
+  } else {
+    // chunks of CH rows staged in LDS, then 16-B coalesced stores of the contiguous block region
+    long long nvalid = P.E - env0;
+    if (nvalid > G) nvalid = G;
+    const int rows = (int)nvalid * N;
+    const int row_id = team * N + t;
+    const int CH = P.chunk_rows;
+    float* dst0 = O.obs + env0 * N * D;
+    for (int c = 0; c < G * N; c += CH) {  // block-uniform trip count
+      if (is_agent && row_id >= c && row_id < c + CH) write_row(stage + (size_t)(row_id - c) * D);
+      __syncthreads();
+      const int nrow = rows - c < CH ? rows - c : CH;
+      if (nrow > 0) {
+        const int total = nrow * D;
+        float* dst = dst0 + (long long)c * D;
+        if (P.obs_vec4) {
+          const int n4 = total >> 2;
+          const float4* s4 = reinterpret_cast<const float4*>(stage);
+          float4* d4 = reinterpret_cast<float4*>(dst);
+          for (int i = tid; i < n4; i += P.threads) d4[i] = s4[i];
+          for (int i = (n4 << 2) + tid; i < total; i += P.threads) dst[i] = stage[i];
+        } else {
+          for (int i = tid; i < total; i += P.threads) dst[i] = stage[i];
+        }
+      }
+      __syncthreads();
     }
   }
 
@@ -651,6 +774,7 @@ int ilog2(int v) {
   while ((1 << r) < v) ++r;
   return r;
 }
+// compile-time slot counts: K+1 (or more) neighbour keys, Ms_eff+1 obstacle keys
 int neighbor_slots(int K) {
   if (K <= 0) return 0;
   if (K <= 3) return 4;
@@ -661,9 +785,9 @@ int neighbor_slots(int K) {
 int obstacle_slots(int Ms, int M) {
   const int need = Ms < M ? Ms : M;
   if (need <= 0) return 0;
-  if (need <= 4) return 4;
-  if (need <= 8) return 8;
-  return 16;
+  if (need <= 4) return 5;
+  if (need <= 8) return 9;
+  return 17;
 }
 
 int obs_dim_of(const swarm_params_t* p) {
@@ -677,7 +801,7 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   if (p->num_envs < 0) return fail(SWARM_EINVAL, "num_envs must be >= 0 (got %d)", p->num_envs);
   if (p->num_drones < 1 || p->num_drones > MAX_N)
     return fail(SWARM_ELIMIT, "num_drones must be in [1, %d] (got %d)", MAX_N, p->num_drones);
-  if (p->num_obstacles < 0) return fail(SWARM_EINVAL, "num_obstacles must be >= 0");
+  if (p->num_obstacles < 0 || p->num_obstacles > 65536) return fail(SWARM_EINVAL, "num_obstacles must be in [0, 65536]");
   if (p->neighbor_k > MAX_K) return fail(SWARM_ELIMIT, "neighbor_k > %d unsupported (got %d)", MAX_K, p->neighbor_k);
   const int msn = p->sensed_obstacles < p->num_obstacles ? p->sensed_obstacles : p->num_obstacles;
   if (msn > MAX_MS) return fail(SWARM_ELIMIT, "sensed_obstacles > %d unsupported (got %d)", MAX_MS, p->sensed_obstacles);
@@ -698,28 +822,34 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   k.Ms = p->sensed_obstacles > 0 ? p->sensed_obstacles : 0;
   k.D = obs_dim_of(p);
   k.max_steps = p->max_steps;
-  k.reward_mode = p->reward_mode;
   k.auto_reset = p->auto_reset ? 1 : 0;
   k.substeps = p->physics_substeps;
   k.damping_law = p->damping_law;
   k.lanes = next_pow2(k.N);
   k.log2_lanes = ilog2(k.lanes);
-  const int threads = k.lanes >= 256 ? k.lanes : 256;
-  k.envs_per_block = threads / k.lanes;
+  const bool wave = k.lanes <= 64;
+  k.threads = wave ? 64 : k.lanes;
+  k.envs_per_block = k.threads / k.lanes;
   const int G = k.envs_per_block;
-  k.pos_stride = k.N + 1;
   k.obst_stride = k.M + 1;
-  const int pos_bytes = G * k.pos_stride * 16;
-  k.off_obst = pos_bytes;
-  k.off_team = k.off_obst + G * k.obst_stride * 16;
-  k.off_block = k.off_team + G * 16;
-  k.off_stage = k.off_block + 16;
-  const long long stage_bytes = (long long)G * k.N * k.D * 4;
-  long long lds = k.off_stage;
-  k.stage_obs = (lds + stage_bytes) <= STAGE_LDS_BUDGET ? 1 : 0;
-  if (k.stage_obs) lds += stage_bytes;
+  k.off_obst = k.threads * 16;
+  const long long obst_bytes = (long long)G * k.obst_stride * 16;
+  k.off_stage = (int)(k.off_obst + obst_bytes);
+  const int rows = G * k.N;
+  const long long row_bytes = 4LL * k.D;
+  int rounds = (int)((rows * row_bytes + STAGE_BUDGET - 1) / STAGE_BUDGET);
+  if (rounds < 1) rounds = 1;
+  int ch = (rows + rounds - 1) / rounds;
+  ch = (ch + 3) & ~3;  // multiple of 4 rows keeps every chunk 16-B aligned
+  if (ch > rows) ch = rows;
+  k.chunk_rows = ch;
+  const long long lds = k.off_stage + (long long)ch * row_bytes;
   if (lds > LDS_LIMIT) return fail(SWARM_ELIMIT, "LDS footprint %lld B exceeds %d B (N=%d, M=%d)", lds, LDS_LIMIT, k.N, k.M);
-  k.obs_vec4 = (((long long)G * k.N * k.D) % 4 == 0) ? 1 : 0;
+  k.obs_vec4 = (((long long)rows * k.D) % 4 == 0 && ((long long)ch * k.D) % 4 == 0) ? 1 : 0;
+  const int nb_bits = ilog2(k.N > 1 ? k.N : 2);
+  const int ob_bits = ilog2(k.M > 1 ? k.M : 2);
+  k.nb_keep = ~((1u << nb_bits) - 1u);
+  k.ob_keep = ~((1u << ob_bits) - 1u);
   k.env_offset = p->env_offset;
   k.seed_lo = (unsigned)(p->seed & 0xffffffffull);
   k.seed_hi = (unsigned)(p->seed >> 32);
@@ -730,6 +860,7 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   k.vmax = (float)p->max_speed;
   k.amax = (float)p->max_accel;
   k.eps_speed = (float)1e-8;
+  k.ds_f = (float)p->desired_spacing;
   k.s_pair = s_threshold((float)(2.0 * p->collision_radius));
   k.s_obst = s_threshold((float)(p->collision_radius + p->obstacle_radius));
   k.s_phys_pair = s_threshold((float)(2.0 * p->drone_contact_radius));
@@ -739,7 +870,6 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   k.g = (float)p->gravity;
   k.gcomp = (float)p->gravity_comp;
   k.goal_radius = p->goal_radius;
-  k.desired_spacing = p->desired_spacing;
   k.kp = p->reward_progress_scale;
   k.r_goal = p->reward_goal;
   k.r_col = p->reward_collision;
@@ -747,7 +877,7 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   k.vmax_d = p->max_speed;
   *kp = k;
   if (info) {
-    info->threads_per_block = threads;
+    info->threads_per_block = k.threads;
     info->envs_per_block = G;
     info->lanes_per_env = k.lanes;
     info->blocks = (int)((k.E + G - 1) / G);
@@ -755,7 +885,7 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
     info->neighbor_slots = neighbor_slots(k.K);
     info->obstacle_slots = obstacle_slots(k.Ms, k.M);
     info->obs_dim = k.D;
-    info->staged_obs = k.stage_obs;
+    info->staged_obs = 1;
   }
   return SWARM_OK;
 }
@@ -763,24 +893,28 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
 typedef void (*kernel_fn)(const KParams, const swarm_state_t, const float*, const uint8_t*, const swarm_out_t,
                           const uint8_t*, int);
 
-template <int DYN, int KS>
+template <int DYN, int KS, bool WAVE>
 kernel_fn pick_ms(int msl) {
   switch (msl) {
-    case 0: return swarm_kernel<DYN, KS, 0>;
-    case 4: return swarm_kernel<DYN, KS, 4>;
-    case 8: return swarm_kernel<DYN, KS, 8>;
-    default: return swarm_kernel<DYN, KS, 16>;
+    case 0: return swarm_kernel<DYN, KS, 0, WAVE>;
+    case 5: return swarm_kernel<DYN, KS, 5, WAVE>;
+    case 9: return swarm_kernel<DYN, KS, 9, WAVE>;
+    default: return swarm_kernel<DYN, KS, 17, WAVE>;
   }
 }
-template <int DYN>
+template <int DYN, bool WAVE>
 kernel_fn pick_ks(int ks, int msl) {
   switch (ks) {
-    case 0: return pick_ms<DYN, 0>(msl);
-    case 4: return pick_ms<DYN, 4>(msl);
-    case 5: return pick_ms<DYN, 5>(msl);
-    case 9: return pick_ms<DYN, 9>(msl);
-    default: return pick_ms<DYN, 17>(msl);
+    case 0: return pick_ms<DYN, 0, WAVE>(msl);
+    case 4: return pick_ms<DYN, 4, WAVE>(msl);
+    case 5: return pick_ms<DYN, 5, WAVE>(msl);
+    case 9: return pick_ms<DYN, 9, WAVE>(msl);
+    default: return pick_ms<DYN, 17, WAVE>(msl);
   }
+}
+kernel_fn pick(int dyn, bool wave, int ks, int msl) {
+  if (dyn == DYN_KIN) return wave ? pick_ks<DYN_KIN, true>(ks, msl) : pick_ks<DYN_KIN, false>(ks, msl);
+  return wave ? pick_ks<DYN_PHYS, true>(ks, msl) : pick_ks<DYN_PHYS, false>(ks, msl);
 }
 
 int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const float* actions, const uint8_t* amask,
@@ -802,8 +936,8 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
       return fail(SWARM_ENULL, "out.reward/terminated/truncated/env_done required by swarm_step");
   }
   if (((uintptr_t)o->obs) % 16 != 0) kp.obs_vec4 = 0;
-  kernel_fn fn = (p->dynamics == DYN_KIN) ? pick_ks<DYN_KIN>(info.neighbor_slots, info.obstacle_slots)
-                                          : pick_ks<DYN_PHYS>(info.neighbor_slots, info.obstacle_slots);
+  const bool wave = kp.lanes <= 64;
+  kernel_fn fn = pick(p->dynamics, wave, info.neighbor_slots, info.obstacle_slots);
   if (info.lds_bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        info.lds_bytes);
