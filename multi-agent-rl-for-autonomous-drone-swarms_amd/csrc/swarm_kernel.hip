@@ -3,17 +3,21 @@
 //
 // A "team" of L = next_pow2(N) lanes owns one env (one lane per drone).
 //   WAVE kernel  (L <= 64): 64-thread workgroups = one wave holding G = 64/L teams.  The N x N
-//                pair pass is symmetric: at rotation r every lane computes the exact squared
-//                distance to drone t+r and receives the one drone t-r computed for it by
-//                ds_bpermute, so each unordered pair is evaluated once.  Team reductions are
-//                wave ballots; no cross-wave barrier exists.
-//   BLOCK kernel (L > 64): one env per workgroup of L threads; ascending broadcast pair loop
-//                from LDS; reductions with __syncthreads_count/or.
-// Both keep the top-(K+1) neighbours as packed 32-bit keys (float bits of the squared distance
-// with the low index bits replaced by the neighbour index) updated by one v_med3_u32 per slot;
-// the survivors are re-ranked by exact distance and an exactness test falls back to a full exact
-// selection in the rare near-tie case, so observations stay bit-exact.
-// Obs rows are staged through a small LDS chunk and stored as 16-B coalesced writes.
+//                pair pass is symmetric: at rotation r lane t evaluates drone t+r and receives,
+//                by ds_bpermute, the value lane t-r evaluated for the pair (t-r, t).  Team
+//                reductions are wave ballots.
+//   BLOCK kernel (L > 64): one env per workgroup of L threads; ascending broadcast pair loop.
+// Step and reset/observe are separate instantiations (KIND) so the step kernel carries no
+// dead paths (SGPR pressure).
+//
+// Ranking vs exactness.  The reference's neighbour distance is
+//   d = sqrtf((float)(((double)(x*x) + (double)(y*y)) + (double)(z*z)))   (OpenBLAS sdot)
+// The pair loop ranks with the cheaper all-float sum s' = ((x*x)+(y*y))+(z*z), which is within
+// 2^-21 relative of the exact s.  Neighbours are kept as packed 32-bit keys (float bits of s'
+// with the low bits replaced by the neighbour index; one v_med3_u32 per slot and insert).  The
+// K+1 survivors are re-ranked with the exact d; a lower bound on every non-survivor proves the
+// top-K exact, else an exact selection runs (rare).  Pair collisions compare the exact nearest
+// distance (all-eligible fast path) or an error-banded running minimum with exact re-check.
 //
 // Bit-exactness: no FP contraction, IEEE sqrt/div where the reference's value is
 // observable, the sdot double-accumulated norm for 1-D norms and the float axis norm for obstacles.
@@ -29,12 +33,39 @@
 
 #pragma clang fp contract(off)
 
+// Diagnostic ablation switches (tools/ablate.sh builds variants; never set in the product build)
+#ifndef SWARM_ABLATE
+#define SWARM_ABLATE 0
+#endif
+#define ABL_PAIR 1     // skip the pair pass
+#define ABL_OBS 2      // skip the observation store
+#define ABL_FINISH 4   // skip the exact top-K re-ranking
+#define ABL_RESET 8    // never auto-reset
+#define ABL_OBST 16    // skip the obstacle pass
+
+// Diagnostic phase timestamps (tools/stamps.py; never set in the product build)
+#ifdef SWARM_STAMPS
+__device__ unsigned long long g_stamps[1 << 20];
+#define STAMP(i)                                                                         \
+  do {                                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+    unsigned long long ts_;                                                              \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");           \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) g_stamps[blockIdx.x * 16 + (i)] = ts_; \
+  } while (0)
+#else
+#define STAMP(i) do {} while (0)
+#endif
+
 namespace {
 
 constexpr uint32_t KEY_EMPTY = 0xffffffffu;
 constexpr int MODE_STEP = 0;
 constexpr int MODE_RESET = 1;
 constexpr int MODE_OBSERVE = 2;
+constexpr int KIND_STEP = 0;
+constexpr int KIND_AUX = 1;  // reset / observe
 constexpr int DYN_KIN = SWARM_DYN_KINEMATIC;
 constexpr int DYN_PHYS = SWARM_DYN_POINTMASS_PHYSICS;
 constexpr int MAX_N = 1024;
@@ -43,19 +74,21 @@ constexpr int MAX_MS = 16;
 constexpr int STAGE_BUDGET = 8 * 1024;  // bytes of LDS for one obs staging chunk
 constexpr int LDS_LIMIT = 160 * 1024;
 constexpr float PAD_POS = 1e18f;        // position of padding lanes (t >= N): never a neighbour
+constexpr float FAST_LO = 1.0f - 0x1p-18f;  // |s' - s| <= 2^-21 s; bands use an 8x margin
+constexpr float FAST_HI = 1.0f + 0x1p-18f;
 
 // Derived, launch-ready parameters (host computes once per call).
 struct KParams {
   int E, N, M, K, Ms, D, max_steps, auto_reset, substeps, damping_law;
-  int lanes, log2_lanes, envs_per_block, threads, chunk_rows, obs_vec4;
-  int off_obst, off_stage, obst_stride;
+  int log2_lanes, envs_per_block, chunk_rows, obs_vec4;
+  int off_obst, off_stage, obst_stride, ring;   // ring: pos4 slots per team (2L wave, L block)
   uint32_t nb_keep, ob_keep;        // key masks: high bits kept from the distance, low bits = index
   long long env_offset;
   unsigned seed_lo, seed_hi;
   float half_w, neg_half_w, width_w;
-  float dt, vmax, amax, eps_speed, ds_f;
-  float s_pair, s_obst;             // kinematic collision thresholds in squared-distance space
-  float s_phys_pair, s_phys_obst, ground_z;
+  float dt, vmax, amax, ds_f;
+  float thr_pair, s_pair, s_obst;   // kinematic: distance threshold, squared-space thresholds
+  float thr_ppair, s_phys_pair, s_phys_obst, ground_z;
   float h, g, gcomp;
   double goal_radius, kp, r_goal, r_col, kf, vmax_d;
 };
@@ -71,10 +104,8 @@ __device__ __forceinline__ float sqsum_1d(float x, float y, float z) {
   const float xx = x * x, yy = y * y, zz = z * z;
   return (float)(((double)xx + (double)yy) + (double)zz);
 }
-// np.linalg.norm(A, axis=1): float32 ((x*x)+(y*y))+(z*z).
-__device__ __forceinline__ float sqsum_axis(float x, float y, float z) {
-  return ((x * x) + (y * y)) + (z * z);
-}
+// np.linalg.norm(A, axis=1): float32 ((x*x)+(y*y))+(z*z).  Also the ranking value s'.
+__device__ __forceinline__ float sqsum_f(float x, float y, float z) { return ((x * x) + (y * y)) + (z * z); }
 
 __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t r;
@@ -87,9 +118,6 @@ __device__ __forceinline__ void kins(uint32_t (&k)[S], uint32_t key) {
 #pragma unroll
   for (int s = S - 1; s > 0; --s) k[s] = med3u(k[s - 1], key, k[s]);
   k[0] = min(k[0], key);
-}
-__device__ __forceinline__ uint32_t pack(float s, uint32_t keep, uint32_t idx) {
-  return (__float_as_uint(s) & keep) | idx;
 }
 
 // ------------------------------------------------------------------ Philox4x32-10 (device reset)
@@ -122,65 +150,90 @@ __device__ __forceinline__ void draw_block(const KParams& P, long long genv, uin
 }
 
 // ------------------------------------------------------------------ pair passes
-// PASS 0: kNN keys only.  PASS 1: kinematic (+ collision and formation over active pairs).
-// PASS 2: physics (+ collision over all real drones).  `self` = this drone's flag (active in
-// kinematic mode, real drone in physics mode); pos4[j].w carries the same flag of drone j.
-template <int KS, int PASS>
-__device__ __forceinline__ void pair_pass_wave(const float4* __restrict__ pos4, int L, int t, int lane0,
-                                               float px, float py, float pz, bool self, uint32_t keep,
-                                               float s_thr, float ds, uint32_t (&nk)[KS > 0 ? KS : 1],
-                                               bool& coll, double& fsum) {
-  const int half = L >> 1;
-  const uint32_t sflag = self ? 0u : 0x80000000u;
-#pragma unroll 2
-  for (int r = 1; r <= half; ++r) {
-    const int j = (t + r) & (L - 1);
-    const float4 q = pos4[j];
-    const float s = sqsum_1d(q.x - px, q.y - py, q.z - pz);
-    const uint32_t sb = __float_as_uint(s);
-    if constexpr (KS > 0) kins<KS>(nk, (sb & keep) | (uint32_t)j);
-    if constexpr (PASS == 1) {
-      const bool pr = self && (q.w != 0.f);
-      coll = coll || (pr && (s <= s_thr));
-      const float e = fabsf(__builtin_amdgcn_sqrtf(s) - ds);
-      fsum += (double)(pr ? e : 0.f);
-    } else if constexpr (PASS == 2) {
-      coll = coll || ((q.w != 0.f) && (s <= s_thr));
-    }
-    if (r < half) {  // mirror: drone m = t-r evaluated the pair (m, t) at this rotation
-      const int m = (t - r) & (L - 1);
-      const uint32_t recv = (uint32_t)__builtin_amdgcn_ds_bpermute((lane0 + m) << 2, (int)(sb | sflag));
-      const uint32_t rb = recv & 0x7fffffffu;
-      if constexpr (KS > 0) kins<KS>(nk, (rb & keep) | (uint32_t)m);
-      if constexpr (PASS == 1) {
-        const bool pr = self && !(recv >> 31);
-        const float sm = __uint_as_float(rb);
-        coll = coll || (pr && (sm <= s_thr));
-        const float e = fabsf(__builtin_amdgcn_sqrtf(sm) - ds);
-        fsum += (double)(pr ? e : 0.f);
-      } else if constexpr (PASS == 2) {
-        coll = coll || (!(recv >> 31) && (__uint_as_float(rb) <= s_thr));
-      }
-    }
+// PASS 0: kNN keys only.  PASS 1: kinematic (+ formation sum, + running min of s' over
+// active pairs unless FAST).  PASS 2: physics (+ running min over real drones unless FAST).
+// FAST: every drone of the wave's teams is eligible (all active / all real, N == L): no masks,
+// pair collisions are decided from the exact nearest neighbour after the pass.
+// `self` = this drone's eligibility; ring[j].w carries drone j's.
+template <int KS, int PASS, bool FAST>
+__device__ __forceinline__ void consume(uint32_t (&nk)[KS > 0 ? KS : 1], float s, uint32_t key_low, bool pr,
+                                        uint32_t keep, float ds, float& smin, float& esum) {
+  if constexpr (KS > 0) kins<KS>(nk, (__float_as_uint(s) & keep) | key_low);
+  if constexpr (PASS != 0 && (!FAST || KS == 0)) smin = fminf(smin, (FAST || pr) ? s : __builtin_inff());
+  if constexpr (PASS == 1) {
+    // formation uses d_ij widened to double in the reference; v_sqrt_f32 of s' keeps the mean
+    // within ~1e-6 relative, far inside the 1e-5 reward contract.
+    const float e = fabsf(__builtin_amdgcn_sqrtf(s) - ds);
+    esum += (FAST || pr) ? e : 0.f;
   }
+}
+
+template <int KS, int PASS, bool FAST>
+__device__ __forceinline__ void pair_pass_wave(const float4* __restrict__ ring, int L, int t, int tid, float px,
+                                               float py, float pz, bool self, uint32_t keep, float ds,
+                                               uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum) {
+  const int half = L >> 1;
+  if (half == 0) return;
+  const uint32_t sflag = (FAST || self) ? 0u : 0x80000000u;
+  const uint32_t lm4 = (uint32_t)(L - 1) << 2;
+  const uint32_t tid4 = (uint32_t)tid << 2;
+  const uint32_t hi4 = tid4 & ~lm4;
+  const uint32_t own0 = (uint32_t)t;        // own key index = t + r   (mod L after the pass)
+  const uint32_t mir0 = (uint32_t)(t + L);  // mirror key index = t + L - r
+  const float4* q0 = ring + t;              // ring holds drone j at j and j + L
+  // Rotations 1 .. half-1 carry a mirror, processed two at a time so that two independent
+  // distance chains and two ds_bpermutes are in flight together.
+  int r = 1;
+  for (; r + 1 < half; r += 2) {
+    const float4 qa = q0[r];
+    const float4 qb = q0[r + 1];
+    const float sa = sqsum_f(qa.x - px, qa.y - py, qa.z - pz);
+    const float sb = sqsum_f(qb.x - px, qb.y - py, qb.z - pz);
+    const uint32_t srca = ((tid4 - ((uint32_t)r << 2)) & lm4) | hi4;  // lane (t - r) mod L
+    const uint32_t srcb = ((tid4 - ((uint32_t)(r + 1) << 2)) & lm4) | hi4;
+    const uint32_t ra = (uint32_t)__builtin_amdgcn_ds_bpermute((int)srca, (int)(__float_as_uint(sa) | sflag));
+    const uint32_t rb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)srcb, (int)(__float_as_uint(sb) | sflag));
+    float esum = 0.f;
+    consume<KS, PASS, FAST>(nk, sa, own0 + (uint32_t)r, self && (qa.w != 0.f), keep, ds, smin, esum);
+    consume<KS, PASS, FAST>(nk, sb, own0 + (uint32_t)(r + 1), self && (qb.w != 0.f), keep, ds, smin, esum);
+    consume<KS, PASS, FAST>(nk, __uint_as_float(ra & 0x7fffffffu), mir0 - (uint32_t)r, self && !(ra >> 31), keep,
+                            ds, smin, esum);
+    consume<KS, PASS, FAST>(nk, __uint_as_float(rb & 0x7fffffffu), mir0 - (uint32_t)(r + 1), self && !(rb >> 31),
+                            keep, ds, smin, esum);
+    if constexpr (PASS == 1) fsum += (double)esum;
+  }
+  float esum = 0.f;
+  if (r < half) {  // odd leftover rotation with a mirror
+    const float4 qa = q0[r];
+    const float sa = sqsum_f(qa.x - px, qa.y - py, qa.z - pz);
+    const uint32_t srca = ((tid4 - ((uint32_t)r << 2)) & lm4) | hi4;
+    const uint32_t ra = (uint32_t)__builtin_amdgcn_ds_bpermute((int)srca, (int)(__float_as_uint(sa) | sflag));
+    consume<KS, PASS, FAST>(nk, sa, own0 + (uint32_t)r, self && (qa.w != 0.f), keep, ds, smin, esum);
+    consume<KS, PASS, FAST>(nk, __uint_as_float(ra & 0x7fffffffu), mir0 - (uint32_t)r, self && !(ra >> 31), keep,
+                            ds, smin, esum);
+  }
+  // r = L/2 pairs t with t+L/2 from both sides: own evaluation only
+  const float4 qh = q0[half];
+  const float sh = sqsum_f(qh.x - px, qh.y - py, qh.z - pz);
+  consume<KS, PASS, FAST>(nk, sh, own0 + (uint32_t)half, self && (qh.w != 0.f), keep, ds, smin, esum);
+  if constexpr (PASS == 1) fsum += (double)esum;
 }
 
 template <int KS, int PASS>
 __device__ __forceinline__ void pair_pass_block(const float4* __restrict__ pos4, int N, int t, float px, float py,
-                                                float pz, bool self, uint32_t keep, float s_thr, float ds,
-                                                uint32_t (&nk)[KS > 0 ? KS : 1], bool& coll, double& fsum) {
+                                                float pz, bool self, uint32_t keep, float ds,
+                                                uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum) {
 #pragma unroll 4
   for (int j = 0; j < N; ++j) {
     const float4 q = pos4[j];
-    const float s = sqsum_1d(q.x - px, q.y - py, q.z - pz);
-    if constexpr (KS > 0) kins<KS>(nk, (j == t) ? KEY_EMPTY : pack(s, keep, (uint32_t)j));
+    const float s = sqsum_f(q.x - px, q.y - py, q.z - pz);
+    const bool other = j != t;
+    if constexpr (KS > 0) kins<KS>(nk, other ? ((__float_as_uint(s) & keep) | (uint32_t)j) : KEY_EMPTY);
+    const bool pr = self && (q.w != 0.f) && other;
+    if constexpr (PASS != 0) smin = fminf(smin, pr ? s : __builtin_inff());
     if constexpr (PASS == 1) {
-      const bool pr = self && (q.w != 0.f) && (j != t);
-      coll = coll || (pr && (s <= s_thr));
       const float e = fabsf(__builtin_amdgcn_sqrtf(s) - ds);
       fsum += (double)(pr ? e : 0.f);
-    } else if constexpr (PASS == 2) {
-      coll = coll || ((j != t) && (s <= s_thr));
     }
   }
 }
@@ -191,55 +244,69 @@ __device__ __forceinline__ void obstacle_pass(const float4* __restrict__ obst4, 
                                               uint32_t (&ok)[MSL > 0 ? MSL : 1], bool& coll) {
   for (int m = 0; m < M; ++m) {
     const float4 q = obst4[m];
-    const float s = sqsum_axis(q.x - px, q.y - py, q.z - pz);
-    if constexpr (MSL > 0) kins<MSL>(ok, pack(s, keep, (uint32_t)m));
+    const float s = sqsum_f(q.x - px, q.y - py, q.z - pz);  // exact axis-path value
+    if constexpr (MSL > 0) kins<MSL>(ok, (__float_as_uint(s) & keep) | (uint32_t)m);
     if constexpr (COLL) coll = coll || (chk && (s <= s_thr));
   }
 }
 
 // Re-rank the S surviving keys by exact distance (the reference sorts by the float distance;
 // ties by index).  Returns false when an entry outside the survivors could still precede the
-// K-th winner (near-tie at truncation granularity) — the caller then runs exact_select.
-template <int S, bool AXIS>
-__device__ __forceinline__ bool finish_keys(const uint32_t (&k)[S], const float4* __restrict__ pts, int count, int K,
-                                            uint32_t keep, float px, float py, float pz, float (&wd)[S],
-                                            int (&wj)[S]) {
+// K-th winner — the caller then runs exact_select.  APPROX: keys hold s' (pairs) rather than the
+// exact value (obstacles), so the non-survivor bound is widened by FAST_LO.
+template <int S, bool AXIS, bool APPROX>
+__device__ __forceinline__ bool finish_keys(const uint32_t (&k)[S], const float4* __restrict__ pts, int count,
+                                            int imod, int K, uint32_t keep, float px, float py, float pz,
+                                            float (&wd)[S], int (&wj)[S]) {
   const uint32_t imask = ~keep;
+  // The keys are already ordered by the (truncated) ranking value; the exact order can differ
+  // only where two survivors lie within the truncation/error band of each other (near-tie,
+  // band 2^-18 relative >> the 1-ulp collapse of sqrt).  Without one, the first K keys are the
+  // answer in order and only their exact distances are needed.
+  bool near = false;
+#pragma unroll
+  for (int s = 0; s + 1 < S; ++s)
+    near = near || (k[s + 1] != KEY_EMPTY &&
+                    __uint_as_float(k[s + 1] & keep) <= __uint_as_float((k[s] & keep) | imask) * FAST_HI);
+  const int need = near ? S : K;
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const uint32_t key = k[s];
-    const int j = (int)(key & imask);
-    const bool valid = (key != KEY_EMPTY) && (j < count);
+    const int j = (int)(key & imask) & imod;
+    const bool valid = (key != KEY_EMPTY) && (j < count) && (s < need);
     float d = __builtin_inff();
     if (valid) {
       const float4 q = pts[j];
-      d = AXIS ? sqrt_rn(sqsum_axis(q.x - px, q.y - py, q.z - pz)) : sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
+      d = AXIS ? sqrt_rn(sqsum_f(q.x - px, q.y - py, q.z - pz)) : sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
     }
     wd[s] = d;
     wj[s] = valid ? j : 0x7fffffff;
   }
+  if (near) {
 #pragma unroll
-  for (int s = 1; s < S; ++s) {
+    for (int s = 1; s < S; ++s) {
 #pragma unroll
-    for (int r = s; r > 0; --r) {
-      const float a = wd[r - 1], b = wd[r];
-      const int ja = wj[r - 1], jb = wj[r];
-      const bool sw = (b < a) || (b == a && jb < ja);
-      wd[r - 1] = sw ? b : a; wd[r] = sw ? a : b;
-      wj[r - 1] = sw ? jb : ja; wj[r] = sw ? ja : jb;
+      for (int r = s; r > 0; --r) {
+        const float a = wd[r - 1], b = wd[r];
+        const int ja = wj[r - 1], jb = wj[r];
+        const bool sw = (b < a) || (b == a && jb < ja);
+        wd[r - 1] = sw ? b : a; wd[r] = sw ? a : b;
+        wj[r - 1] = sw ? jb : ja; wj[r] = sw ? ja : jb;
+      }
     }
   }
   const uint32_t last = k[S - 1];
-  if (last == KEY_EMPTY || (int)(last & imask) >= count) return true;
+  if (last == KEY_EMPTY || (int)((last & imask) & imod) >= count) return true;
   if (K <= 0) return true;
-  const float dlb = sqrt_rn(__uint_as_float(last & keep));
+  const float base = __uint_as_float(last & keep);
+  const float dlb = sqrt_rn(APPROX ? base * FAST_LO : base);
   return dlb > wd[K - 1];
 }
 
 // Exact (distance, index) selection of the K nearest of `count` points (rare fallback).
 template <int S, bool AXIS>
 __device__ __forceinline__ void exact_select(const float4* __restrict__ pts, int count, int self, int K, float px,
-                                          float py, float pz, float (&wd)[S], int (&wj)[S]) {
+                                             float py, float pz, float (&wd)[S], int (&wj)[S]) {
   float pd = -1.f;
   int pj = -1;
 #pragma unroll
@@ -250,7 +317,7 @@ __device__ __forceinline__ void exact_select(const float4* __restrict__ pts, int
       for (int j = 0; j < count; ++j) {
         if (j == self) continue;
         const float4 q = pts[j];
-        const float d = AXIS ? sqrt_rn(sqsum_axis(q.x - px, q.y - py, q.z - pz))
+        const float d = AXIS ? sqrt_rn(sqsum_f(q.x - px, q.y - py, q.z - pz))
                              : sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
         const bool gt = (d > pd) || (d == pd && j > pj);
         const bool lt = (d < bd) || (d == bd && j < bj);
@@ -264,15 +331,32 @@ __device__ __forceinline__ void exact_select(const float4* __restrict__ pts, int
   }
 }
 
+// exact "any eligible pair within s_thr" (fallback of the banded running minimum)
+__device__ __forceinline__ bool exact_pair_collision(const float4* __restrict__ pts, int count, int self,
+                                                     float px, float py, float pz, float s_thr) {
+  bool c = false;
+  for (int j = 0; j < count; ++j) {
+    const float4 q = pts[j];
+    if (j != self && q.w != 0.f) c = c || (sqsum_1d(q.x - px, q.y - py, q.z - pz) <= s_thr);
+  }
+  return c;
+}
+
 // ------------------------------------------------------------------ the kernel
-template <int DYN, int KS, int MSL, bool WAVE>
+template <int KIND, int DYN, int KS, int MSL, bool WAVE>
 __global__ void __launch_bounds__(WAVE ? 64 : 1024)
 swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ actions,
              const uint8_t* __restrict__ amask, const swarm_out_t O,
-             const uint8_t* __restrict__ env_mask, int mode) {
+             const uint8_t* __restrict__ env_mask, int mode_arg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // compile-time mode in the step kernel; reset/observe share the aux kernel
+  const int mode = (KIND == KIND_STEP) ? MODE_STEP : (mode_arg == MODE_RESET ? MODE_RESET : MODE_OBSERVE);
+  STAMP(0);
+#ifdef SWARM_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) g_stamps[blockIdx.x * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+#endif
   const int tid = threadIdx.x;
-  const int L = P.lanes;
+  const int L = 1 << P.log2_lanes;
   const int team = tid >> P.log2_lanes;
   const int t = tid & (L - 1);
   const int G = P.envs_per_block;
@@ -281,12 +365,11 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   const long long env = env0 + team;
   const bool env_ok = env < P.E;
   const bool is_agent = env_ok && t < N;
-  const int lane0 = team * L;  // first thread of this team
-  float4* pos4 = reinterpret_cast<float4*>(smem) + lane0;
+  float4* ring = reinterpret_cast<float4*>(smem) + team * P.ring;
   float4* obst4 = reinterpret_cast<float4*>(smem + P.off_obst) + team * P.obst_stride;
   float* stage = reinterpret_cast<float*>(smem + P.off_stage);
   uint64_t team_bits = 0;
-  if constexpr (WAVE) team_bits = (L == 64) ? ~0ull : (((1ull << L) - 1ull) << lane0);
+  if constexpr (WAVE) team_bits = (L == 64) ? ~0ull : (((1ull << L) - 1ull) << (team * L));
 
   // envs this call writes: every env (step) or the masked ones (reset / observe)
   bool sel = env_ok;
@@ -303,28 +386,37 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     gx = S.goal[env * 3 + 0];
     gy = S.goal[env * 3 + 1];
     gz = S.goal[env * 3 + 2];
-    stepc = S.step_count[env];
+    if (mode == MODE_STEP) stepc = S.step_count[env];
   }
   float px = PAD_POS, py = PAD_POS, pz = PAD_POS, vx = 0.f, vy = 0.f, vz = 0.f, damp = 0.f;
   bool act = false;
   const long long ag = env * N + t;
+  float ax = 0.f, ay = 0.f, az = 0.f;
+  bool has = true;
   if (is_agent) {
+    if (mode == MODE_STEP) {
+      ax = actions[ag * 3 + 0]; ay = actions[ag * 3 + 1]; az = actions[ag * 3 + 2];
+      has = (amask == nullptr) || (amask[ag] != 0);
+    }
     px = S.pos[ag * 3 + 0]; py = S.pos[ag * 3 + 1]; pz = S.pos[ag * 3 + 2];
     vx = S.vel[ag * 3 + 0]; vy = S.vel[ag * 3 + 1]; vz = S.vel[ag * 3 + 2];
     act = S.active[ag] != 0;
-    if constexpr (DYN == DYN_PHYS) damp = S.damping[ag];
+    if constexpr (DYN == DYN_PHYS) {
+      if (mode == MODE_STEP) damp = S.damping[ag];
+    }
   }
-  int n_active;
-  if constexpr (WAVE) n_active = __popcll(__ballot(is_agent && act) & team_bits);
-  else n_active = __syncthreads_count(is_agent && act);
+  int n_active = 0;
+  if (mode == MODE_STEP) {
+    if constexpr (WAVE) n_active = __popcll(__ballot(is_agent && act) & team_bits);
+    else n_active = __syncthreads_count(is_agent && act);
+  }
 
   // ---- integrate (step) or draw (explicit reset)
+  STAMP(1);
   float prev_d = 0.f;
   uint32_t episode_new = 0;
   const long long genv = P.env_offset + env;
   if (mode == MODE_STEP && is_agent) {
-    float ax = actions[ag * 3 + 0], ay = actions[ag * 3 + 1], az = actions[ag * 3 + 2];
-    const bool has = (amask == nullptr) || (amask[ag] != 0);
     if constexpr (DYN == DYN_KIN) {
       if (act) {  // drone_swarm_env.py:98-111
         prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
@@ -336,7 +428,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         vy = vy + ay * P.dt;
         vz = vz + az * P.dt;
         const float sp = sqrt_rn(sqsum_1d(vx, vy, vz));  // _clip_speed :179-183
-        if (!(sp <= P.vmax || sp < P.eps_speed)) {
+        if (!(sp <= P.vmax || sp < (float)1e-8)) {
           vx = (vx / sp) * P.vmax;
           vy = (vy / sp) * P.vmax;
           vz = (vz / sp) * P.vmax;
@@ -384,9 +476,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     }
   }
 
-  // explicit device reset: draw the new episode before the observation pass
-  if (mode == MODE_RESET && sel) {
-    episode_new = S.episode[env] + 1u;
+  auto draw_env = [&]() {  // new episode for this team (drone_swarm_env.py:72-80 ranges)
     uint32_t w[4];
     if (t < N) {
       draw_block(P, genv, episode_new, (uint32_t)t, w);
@@ -411,42 +501,85 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     gy = uni(w[1], P.neg_half_w, P.width_w);
     gz = uni(w[2], P.neg_half_w, P.width_w);
     if constexpr (DYN == DYN_PHYS) gz = uni(w[3], 0.5f, 1.5f);
+  };
+  auto put_ring = [&](float w) {
+    ring[t] = make_float4(px, py, pz, w);
+    if constexpr (WAVE) ring[t + L] = make_float4(px, py, pz, w);
+  };
+
+  if (mode == MODE_RESET && sel) {  // explicit device reset: draw before the observation pass
+    episode_new = S.episode[env] + 1u;
+    draw_env();
     stepc = 0;
   }
 
-  // LDS slot: (p, flag); padding lanes sit far away with flag 0
-  const float wflag = (DYN == DYN_KIN) ? (act ? 1.f : 0.f) : (is_agent ? 1.f : 0.f);
-  pos4[t] = make_float4(px, py, pz, wflag);
+  STAMP(2);
+  // LDS slot: (p, eligibility); padding lanes sit far away with flag 0
+  const bool elig = (DYN == DYN_KIN) ? act : is_agent;
+  put_ring(elig ? 1.f : 0.f);
   __syncthreads();
 
   // ---- pair + obstacle passes
-  uint32_t nk[KS > 0 ? KS : 1];
-  uint32_t ok[MSL > 0 ? MSL : 1];
+  constexpr int NW = KS > 0 ? KS : 1;
+  constexpr int OW = MSL > 0 ? MSL : 1;
+  uint32_t nk[NW];
+  uint32_t ok[OW];
 #pragma unroll
-  for (int s = 0; s < (KS > 0 ? KS : 1); ++s) nk[s] = KEY_EMPTY;
+  for (int s = 0; s < NW; ++s) nk[s] = KEY_EMPTY;
 #pragma unroll
-  for (int s = 0; s < (MSL > 0 ? MSL : 1); ++s) ok[s] = KEY_EMPTY;
-  bool coll = false;
+  for (int s = 0; s < OW; ++s) ok[s] = KEY_EMPTY;
+  bool ocoll = false;
+  float smin = __builtin_inff();  // running min of s' over eligible pairs (banded)
   double fsum = 0.0;
   const bool pass_env = (mode == MODE_STEP) ? env_ok : sel;
-  const bool self_flag = (DYN == DYN_KIN) ? act : is_agent;
-  if (pass_env) {
+  // all-eligible fast path: wave-uniform, needs the nearest neighbour (KS > 0) and no padding
+  bool fast = false;
+  if constexpr (WAVE) fast = (KS > 0) && (N == L) && __all(elig);
+  if (pass_env && !(SWARM_ABLATE & ABL_PAIR)) {
     if (mode == MODE_STEP) {
-      if constexpr (DYN == DYN_KIN) {
-        if constexpr (WAVE) pair_pass_wave<KS, 1>(pos4, L, t, lane0, px, py, pz, self_flag, P.nb_keep, P.s_pair, P.ds_f, nk, coll, fsum);
-        else pair_pass_block<KS, 1>(pos4, N, t, px, py, pz, self_flag, P.nb_keep, P.s_pair, P.ds_f, nk, coll, fsum);
-        obstacle_pass<MSL, true>(obst4, M, px, py, pz, act, P.s_obst, P.ob_keep, ok, coll);
+      constexpr int PASS = (DYN == DYN_KIN) ? 1 : 2;
+      if constexpr (WAVE) {
+        if (fast) pair_pass_wave<KS, PASS, true>(ring, L, t, tid, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
+        else pair_pass_wave<KS, PASS, false>(ring, L, t, tid, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
       } else {
-        if constexpr (WAVE) pair_pass_wave<KS, 2>(pos4, L, t, lane0, px, py, pz, self_flag, P.nb_keep, P.s_phys_pair, 0.f, nk, coll, fsum);
-        else pair_pass_block<KS, 2>(pos4, N, t, px, py, pz, self_flag, P.nb_keep, P.s_phys_pair, 0.f, nk, coll, fsum);
-        obstacle_pass<MSL, true>(obst4, M, px, py, pz, true, P.s_phys_obst, P.ob_keep, ok, coll);
+        pair_pass_block<KS, PASS>(ring, N, t, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
       }
+      if constexpr (SWARM_ABLATE & ABL_OBST) {}
+      else if constexpr (DYN == DYN_KIN) obstacle_pass<MSL, true>(obst4, M, px, py, pz, act, P.s_obst, P.ob_keep, ok, ocoll);
+      else obstacle_pass<MSL, true>(obst4, M, px, py, pz, true, P.s_phys_obst, P.ob_keep, ok, ocoll);
     } else {
-      if constexpr (WAVE) pair_pass_wave<KS, 0>(pos4, L, t, lane0, px, py, pz, self_flag, P.nb_keep, 0.f, 0.f, nk, coll, fsum);
-      else pair_pass_block<KS, 0>(pos4, N, t, px, py, pz, self_flag, P.nb_keep, 0.f, 0.f, nk, coll, fsum);
-      obstacle_pass<MSL, false>(obst4, M, px, py, pz, false, 0.f, P.ob_keep, ok, coll);
+      if constexpr (WAVE) pair_pass_wave<KS, 0, true>(ring, L, t, tid, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
+      else pair_pass_block<KS, 0>(ring, N, t, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
+      obstacle_pass<MSL, false>(obst4, M, px, py, pz, false, 0.f, P.ob_keep, ok, ocoll);
     }
   }
+
+  STAMP(3);
+  // ---- exact top-K for the current (post-step) state
+  float wd[NW], od[OW];
+  int wj[NW], oj[OW];
+#pragma unroll
+  for (int s = 0; s < NW; ++s) { wd[s] = 0.f; wj[s] = 0x7fffffff; }
+#pragma unroll
+  for (int s = 0; s < OW; ++s) { od[s] = 0.f; oj[s] = 0x7fffffff; }
+  const int imod = WAVE ? (L - 1) : 0x7fffffff;
+  const int Kq = (fast && K < 1) ? 1 : K;  // the fast collision test needs the nearest
+  const int Mse = Ms < M ? Ms : M;
+  auto select_topk = [&](bool run) {
+    bool slow_nb = false, slow_ob = false;
+    if (run && !(SWARM_ABLATE & ABL_FINISH)) {
+      if constexpr (KS > 0) slow_nb = !finish_keys<KS, false, true>(nk, ring, N, imod, Kq, P.nb_keep, px, py, pz, wd, wj);
+      if constexpr (MSL > 0) slow_ob = !finish_keys<MSL, true, false>(ok, obst4, M, 0x7fffffff, Mse, P.ob_keep, px, py, pz, od, oj);
+    }
+    if constexpr (KS > 0) {
+      if (slow_nb) exact_select<NW, false>(ring, N, t, Kq, px, py, pz, wd, wj);
+    }
+    if constexpr (MSL > 0) {
+      if (slow_ob) exact_select<OW, true>(obst4, M, -1, Mse, px, py, pz, od, oj);
+    }
+  };
+  select_topk(is_agent && pass_env);
+  STAMP(4);
 
   // ---- rewards / terminations (step)
   float rew = 0.f, dist_out = 0.f;
@@ -456,12 +589,22 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   if (mode == MODE_STEP) {
     bool p_coll = false, p_cand = false, p_notall = false;
     if (is_agent) {
+      // pair collision: exact nearest (fast) or banded running minimum with exact re-check
+      const float s_exact_thr = (DYN == DYN_KIN) ? P.s_pair : P.s_phys_pair;
+      bool pcoll;
+      if (fast) {
+        pcoll = wd[0] <= ((DYN == DYN_KIN) ? P.thr_pair : P.thr_ppair);
+      } else {
+        pcoll = smin <= s_exact_thr * FAST_LO;
+        if (!pcoll && smin <= s_exact_thr * FAST_HI && elig)
+          pcoll = exact_pair_collision(ring, N, t, px, py, pz, s_exact_thr);
+      }
       if constexpr (DYN == DYN_KIN) {
         const float curr = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
         dist_out = curr;
         if (act) {
           reached = (double)curr <= P.goal_radius;  // fp64 compare, :124-127
-          collided = coll;
+          collided = ocoll || pcoll;
           p_coll = collided;
           p_cand = !reached && !collided;
           double r = ((double)prev_d - (double)curr) * P.kp;
@@ -476,7 +619,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         const double dz = (double)pz - (double)gz;
         const double dist_phys = dsqrt_rn(((dx * dx) + (dy * dy)) + (dz * dz));
         dist_out = (float)dist_phys;
-        collided = coll || (pz <= P.ground_z);
+        collided = ocoll || pcoll || (pz <= P.ground_z);
         reached = dist_phys < P.goal_radius;
         if (act) {
           p_coll = collided;
@@ -525,165 +668,10 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       trunc = trunc_all;
       cont = true;
     }
-    do_reset = P.auto_reset && env_ok && (term_all || trunc_all);
-    bool any_reset;
-    if constexpr (WAVE) any_reset = __ballot(do_reset) != 0;
-    else any_reset = __syncthreads_or(do_reset) != 0;
-    if (any_reset) {  // block-uniform: some team re-draws its env in-kernel
-      __syncthreads();  // pass-1 reads of pos4/obst4 are done
-      if (do_reset) {
-        episode_new = S.episode[env] + 1u;
-        uint32_t w[4];
-        if (t < N) {
-          draw_block(P, genv, episode_new, (uint32_t)t, w);
-          px = uni(w[0], P.neg_half_w, P.width_w);
-          py = uni(w[1], P.neg_half_w, P.width_w);
-          pz = uni(w[2], P.neg_half_w, P.width_w);
-          if constexpr (DYN == DYN_PHYS) {
-            pz = fmaxf(pz, 1.0f);
-            damp = 0.5f * uni(w[3], 0.8f, 0.4f);
-          }
-          vx = vy = vz = 0.f;
-          pos4[t] = make_float4(px, py, pz, 1.f);
-        }
-        for (int m = t; m < M; m += L) {
-          draw_block(P, genv, episode_new, (uint32_t)(N + m), w);
-          float oz = uni(w[2], P.neg_half_w, P.width_w);
-          if constexpr (DYN == DYN_PHYS) oz = fmaxf(oz, 0.5f);
-          obst4[m] = make_float4(uni(w[0], P.neg_half_w, P.width_w), uni(w[1], P.neg_half_w, P.width_w), oz, 0.f);
-        }
-        draw_block(P, genv, episode_new, (uint32_t)(N + M), w);
-        gx = uni(w[0], P.neg_half_w, P.width_w);
-        gy = uni(w[1], P.neg_half_w, P.width_w);
-        gz = uni(w[2], P.neg_half_w, P.width_w);
-        if constexpr (DYN == DYN_PHYS) gz = uni(w[3], 0.5f, 1.5f);
-      }
-      __syncthreads();
-      if (do_reset) {
-#pragma unroll
-        for (int s = 0; s < (KS > 0 ? KS : 1); ++s) nk[s] = KEY_EMPTY;
-#pragma unroll
-        for (int s = 0; s < (MSL > 0 ? MSL : 1); ++s) ok[s] = KEY_EMPTY;
-        bool c2 = false;
-        double f2 = 0.0;
-        const bool fl = t < N;
-        if constexpr (WAVE) pair_pass_wave<KS, 0>(pos4, L, t, lane0, px, py, pz, fl, P.nb_keep, 0.f, 0.f, nk, c2, f2);
-        else pair_pass_block<KS, 0>(pos4, N, t, px, py, pz, fl, P.nb_keep, 0.f, 0.f, nk, c2, f2);
-        obstacle_pass<MSL, false>(obst4, M, px, py, pz, false, 0.f, P.ob_keep, ok, c2);
-      }
-    }
-  } else if (sel && is_agent) {
-    dist_out = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
-  }
+    do_reset = P.auto_reset && env_ok && (term_all || trunc_all) && !(SWARM_ABLATE & ABL_RESET);
 
-  // ---- exact neighbour / obstacle selection for the observation
-  const bool write_env = (mode == MODE_STEP) ? env_ok : sel;
-  constexpr int NW = KS > 0 ? KS : 1;
-  constexpr int OW = MSL > 0 ? MSL : 1;
-  float wd[NW], od[OW];
-  int wj[NW], oj[OW];
-#pragma unroll
-  for (int s = 0; s < NW; ++s) { wd[s] = 0.f; wj[s] = 0x7fffffff; }
-#pragma unroll
-  for (int s = 0; s < OW; ++s) { od[s] = 0.f; oj[s] = 0x7fffffff; }
-  bool slow_nb = false, slow_ob = false;
-  if (is_agent && write_env) {
-    if constexpr (KS > 0) slow_nb = !finish_keys<KS, false>(nk, pos4, N, K, P.nb_keep, px, py, pz, wd, wj);
-    if constexpr (MSL > 0) slow_ob = !finish_keys<MSL, true>(ok, obst4, M, Ms < M ? Ms : M, P.ob_keep, px, py, pz, od, oj);
-  }
-  if constexpr (KS > 0) {
-    if (slow_nb) exact_select<NW, false>(pos4, N, t, K, px, py, pz, wd, wj);
-  }
-  if constexpr (MSL > 0) {
-    if (slow_ob) exact_select<OW, true>(obst4, M, -1, Ms < M ? Ms : M, px, py, pz, od, oj);
-  }
-
-  // observation velocity (physics clamps it in the obs only, drone_physics_env.py:438-442)
-  float ovx = vx, ovy = vy, ovz = vz;
-  if constexpr (DYN == DYN_PHYS) {
-    const double dvx = (double)vx, dvy = (double)vy, dvz = (double)vz;
-    const double nv = dsqrt_rn(((dvx * dvx) + (dvy * dvy)) + (dvz * dvz));
-    if (nv > P.vmax_d) {
-      ovx = (float)((dvx / nv) * P.vmax_d);
-      ovy = (float)((dvy / nv) * P.vmax_d);
-      ovz = (float)((dvz / nv) * P.vmax_d);
-    }
-  }
-
-  // ---- observation rows: [p | v | g-p | K x (p_j-p_i, d) | Ms x (o_m-p_i, d)]
-  auto write_row = [&](float* row) {
-    row[0] = px; row[1] = py; row[2] = pz;
-    row[3] = ovx; row[4] = ovy; row[5] = ovz;
-    row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
-    int col = 9;
-    if constexpr (KS > 0) {
-#pragma unroll
-      for (int s = 0; s < KS - 1; ++s) {
-        if (s < K) {
-          float f0 = 0.f, f1 = 0.f, f2 = 0.f, f3 = 0.f;
-          if (wj[s] < N) {
-            const float4 q = pos4[wj[s]];
-            f0 = q.x - px; f1 = q.y - py; f2 = q.z - pz; f3 = wd[s];
-          }
-          row[col + 4 * s + 0] = f0; row[col + 4 * s + 1] = f1;
-          row[col + 4 * s + 2] = f2; row[col + 4 * s + 3] = f3;
-        }
-      }
-    }
-    col += 4 * K;
-    for (int s = 0; s < Ms; ++s) {
-      float f0 = 0.f, f1 = 0.f, f2 = 0.f, f3 = 0.f;
-      int m = 0x7fffffff;
-      float d = 0.f;
-      if constexpr (MSL > 0) {
-#pragma unroll
-        for (int u = 0; u < MSL - 1; ++u)
-          if (u == s) { m = oj[u]; d = od[u]; }
-      }
-      if (m < M) {
-        const float4 q = obst4[m];
-        f0 = q.x - px; f1 = q.y - py; f2 = q.z - pz; f3 = d;
-      }
-      row[col + 4 * s + 0] = f0; row[col + 4 * s + 1] = f1;
-      row[col + 4 * s + 2] = f2; row[col + 4 * s + 3] = f3;
-    }
-  };
-
-  if (mode != MODE_STEP && env_mask != nullptr) {
-    // masked reset/observe: rows straight to global memory (off the hot path)
-    if (is_agent && sel) write_row(O.obs + (size_t)ag * D);
-  } else {
-    // chunks of CH rows staged in LDS, then 16-B coalesced stores of the contiguous block region
-    long long nvalid = P.E - env0;
-    if (nvalid > G) nvalid = G;
-    const int rows = (int)nvalid * N;
-    const int row_id = team * N + t;
-    const int CH = P.chunk_rows;
-    float* dst0 = O.obs + env0 * N * D;
-    for (int c = 0; c < G * N; c += CH) {  // block-uniform trip count
-      if (is_agent && row_id >= c && row_id < c + CH) write_row(stage + (size_t)(row_id - c) * D);
-      __syncthreads();
-      const int nrow = rows - c < CH ? rows - c : CH;
-      if (nrow > 0) {
-        const int total = nrow * D;
-        float* dst = dst0 + (long long)c * D;
-        if (P.obs_vec4) {
-          const int n4 = total >> 2;
-          const float4* s4 = reinterpret_cast<const float4*>(stage);
-          float4* d4 = reinterpret_cast<float4*>(dst);
-          for (int i = tid; i < n4; i += P.threads) d4[i] = s4[i];
-          for (int i = (n4 << 2) + tid; i < total; i += P.threads) dst[i] = stage[i];
-        } else {
-          for (int i = tid; i < total; i += P.threads) dst[i] = stage[i];
-        }
-      }
-      __syncthreads();
-    }
-  }
-
-  // ---- per-agent outputs and state write-back
-  if (is_agent) {
-    if (mode == MODE_STEP) {
+    // per-agent step outputs (the episode that just ended, for reset envs)
+    if (is_agent) {
       O.reward[ag] = rew;
       O.terminated[ag] = term ? 1 : 0;
       O.truncated[ag] = trunc ? 1 : 0;
@@ -691,6 +679,46 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       if (O.info_flags)
         O.info_flags[ag] = (uint8_t)((act ? SWARM_AGENT_STEPPED : 0u) | (act && reached ? SWARM_AGENT_REACHED : 0u) |
                                      (act && collided ? SWARM_AGENT_COLLISION : 0u) | (cont ? SWARM_AGENT_HAS_OBS : 0u));
+    }
+    if (env_ok && t == 0)
+      O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
+                                  (do_reset ? SWARM_ENV_RESET : 0u));
+
+    STAMP(5);
+    bool any_reset;
+    if constexpr (WAVE) any_reset = __ballot(do_reset) != 0;
+    else any_reset = __syncthreads_or(do_reset) != 0;
+    if (any_reset) {  // block-uniform: some team re-draws its env in-kernel
+      __syncthreads();  // pass-1 reads of ring/obst4 are done
+      if (do_reset) {
+        episode_new = S.episode[env] + 1u;
+        draw_env();
+        put_ring(1.f);
+      }
+      __syncthreads();
+      if (do_reset) {
+#pragma unroll
+        for (int s = 0; s < NW; ++s) nk[s] = KEY_EMPTY;
+#pragma unroll
+        for (int s = 0; s < OW; ++s) ok[s] = KEY_EMPTY;
+        bool c2 = false;
+        float s2 = 0.f;
+        double f2 = 0.0;
+        if constexpr (WAVE) pair_pass_wave<KS, 0, true>(ring, L, t, tid, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
+        else pair_pass_block<KS, 0>(ring, N, t, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
+        obstacle_pass<MSL, false>(obst4, M, px, py, pz, false, 0.f, P.ob_keep, ok, c2);
+      }
+      select_topk(do_reset && is_agent);
+    }
+  } else if (sel && is_agent) {
+    dist_out = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
+  }
+
+  STAMP(6);
+  // ---- state write-back
+  const bool write_env = (mode == MODE_STEP) ? env_ok : sel;
+  if (is_agent) {
+    if (mode == MODE_STEP) {
       bool new_act;
       if constexpr (DYN == DYN_KIN) new_act = cont;
       else new_act = act && !(term_all || trunc_all);
@@ -717,13 +745,8 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   }
   const bool new_episode = (mode == MODE_STEP) ? do_reset : (mode == MODE_RESET && sel);
   if (env_ok && t == 0) {
-    if (mode == MODE_STEP) {
-      O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
-                                  (do_reset ? SWARM_ENV_RESET : 0u));
-      S.step_count[env] = do_reset ? 0 : new_step;
-    } else if (mode == MODE_RESET && sel) {
-      S.step_count[env] = 0;
-    }
+    if (mode == MODE_STEP) S.step_count[env] = do_reset ? 0 : new_step;
+    else if (mode == MODE_RESET && sel) S.step_count[env] = 0;
     if (new_episode) {
       S.episode[env] = episode_new;
       S.goal[env * 3 + 0] = gx; S.goal[env * 3 + 1] = gy; S.goal[env * 3 + 2] = gz;
@@ -736,6 +759,105 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       o[0] = q.x; o[1] = q.y; o[2] = q.z;
     }
   }
+
+  STAMP(7);
+  // observation velocity (physics clamps it in the obs only, drone_physics_env.py:438-442)
+  float ovx = vx, ovy = vy, ovz = vz;
+  if constexpr (DYN == DYN_PHYS) {
+    const double dvx = (double)vx, dvy = (double)vy, dvz = (double)vz;
+    const double nv = dsqrt_rn(((dvx * dvx) + (dvy * dvy)) + (dvz * dvz));
+    if (nv > P.vmax_d) {
+      ovx = (float)((dvx / nv) * P.vmax_d);
+      ovy = (float)((dvy / nv) * P.vmax_d);
+      ovz = (float)((dvz / nv) * P.vmax_d);
+    }
+  }
+
+  // ---- observation rows: [p | v | g-p | K x (p_j-p_i, d) | Ms x (o_m-p_i, d)]
+  auto write_row = [&](float* row) {
+    row[0] = px; row[1] = py; row[2] = pz;
+    row[3] = ovx; row[4] = ovy; row[5] = ovz;
+    row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
+    int col = 9;
+    if constexpr (KS > 0) {
+#pragma unroll
+      for (int s = 0; s < KS - 1; ++s) {
+        if (s < K) {
+          float f0 = 0.f, f1 = 0.f, f2 = 0.f, f3 = 0.f;
+          if (wj[s] < N) {
+            const float4 q = ring[wj[s]];
+            f0 = q.x - px; f1 = q.y - py; f2 = q.z - pz; f3 = wd[s];
+          }
+          row[col + 4 * s + 0] = f0; row[col + 4 * s + 1] = f1;
+          row[col + 4 * s + 2] = f2; row[col + 4 * s + 3] = f3;
+        }
+      }
+    }
+    col += 4 * K;
+    for (int s = 0; s < Ms; ++s) {
+      float f0 = 0.f, f1 = 0.f, f2 = 0.f, f3 = 0.f;
+      int m = 0x7fffffff;
+      float d = 0.f;
+      if constexpr (MSL > 0) {
+#pragma unroll
+        for (int u = 0; u < MSL - 1; ++u)
+          if (u == s) { m = oj[u]; d = od[u]; }
+      }
+      if (m < M) {
+        const float4 q = obst4[m];
+        f0 = q.x - px; f1 = q.y - py; f2 = q.z - pz; f3 = d;
+      }
+      row[col + 4 * s + 0] = f0; row[col + 4 * s + 1] = f1;
+      row[col + 4 * s + 2] = f2; row[col + 4 * s + 3] = f3;
+    }
+  };
+
+  if (SWARM_ABLATE & ABL_OBS) {
+  } else if (mode != MODE_STEP && env_mask != nullptr) {
+    // masked reset/observe: rows straight to global memory (off the hot path)
+    if (is_agent && sel) write_row(O.obs + (size_t)ag * D);
+  } else {
+    // chunks of CH rows staged in LDS, then 16-B coalesced stores of the contiguous block region
+    long long nvalid = P.E - env0;
+    if (nvalid > G) nvalid = G;
+    const int rows = (int)nvalid * N;
+    const int row_id = team * N + t;
+    const int CH = P.chunk_rows;
+    const int nthr = blockDim.x;
+    float* dst0 = O.obs + env0 * N * D;
+    for (int c = 0; c < G * N; c += CH) {  // block-uniform trip count
+      if (is_agent && row_id >= c && row_id < c + CH) write_row(stage + (size_t)(row_id - c) * D);
+      __syncthreads();
+      const int nrow = rows - c < CH ? rows - c : CH;
+      if (nrow > 0) {
+        const int total = nrow * D;
+        float* dst = dst0 + (long long)c * D;
+        if (P.obs_vec4) {
+          const int n4 = total >> 2;
+          const float4* s4 = reinterpret_cast<const float4*>(stage);
+          float4* d4 = reinterpret_cast<float4*>(dst);
+          int i = tid;
+          for (; i + 3 * nthr < n4; i += 4 * nthr) {
+            const float4 a0 = s4[i], a1 = s4[i + nthr], a2 = s4[i + 2 * nthr], a3 = s4[i + 3 * nthr];
+            d4[i] = a0; d4[i + nthr] = a1; d4[i + 2 * nthr] = a2; d4[i + 3 * nthr] = a3;
+          }
+          for (; i < n4; i += nthr) d4[i] = s4[i];
+          for (int i = (n4 << 2) + tid; i < total; i += nthr) dst[i] = stage[i];
+        } else {
+          for (int i = tid; i < total; i += nthr) dst[i] = stage[i];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  STAMP(8);
+#ifdef SWARM_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) {
+    g_stamps[blockIdx.x * 16 + 9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+    g_stamps[blockIdx.x * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    g_stamps[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 // ------------------------------------------------------------------ host side
@@ -749,7 +871,7 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
-// Largest float s >= 0 with sqrtf(s) <= T: lets the pair loop compare the exact float squared
+// Largest float s >= 0 with sqrtf(s) <= T: lets the passes compare the exact float squared
 // sum instead of taking a correctly rounded sqrt per pair, with identical outcomes.
 float s_threshold(float T) {
   if (!(T >= 0.0f)) return -1.0f;
@@ -778,7 +900,6 @@ int ilog2(int v) {
 int neighbor_slots(int K) {
   if (K <= 0) return 0;
   if (K <= 3) return 4;
-  if (K == 4) return 5;
   if (K <= 8) return 9;
   return 17;
 }
@@ -825,14 +946,15 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   k.auto_reset = p->auto_reset ? 1 : 0;
   k.substeps = p->physics_substeps;
   k.damping_law = p->damping_law;
-  k.lanes = next_pow2(k.N);
-  k.log2_lanes = ilog2(k.lanes);
-  const bool wave = k.lanes <= 64;
-  k.threads = wave ? 64 : k.lanes;
-  k.envs_per_block = k.threads / k.lanes;
+  const int lanes = next_pow2(k.N);
+  k.log2_lanes = ilog2(lanes);
+  const bool wave = lanes <= 64;
+  const int threads = wave ? 64 : lanes;
+  k.envs_per_block = threads / lanes;
   const int G = k.envs_per_block;
+  k.ring = wave ? 2 * lanes : lanes;
   k.obst_stride = k.M + 1;
-  k.off_obst = k.threads * 16;
+  k.off_obst = G * k.ring * 16;
   const long long obst_bytes = (long long)G * k.obst_stride * 16;
   k.off_stage = (int)(k.off_obst + obst_bytes);
   const int rows = G * k.N;
@@ -846,9 +968,10 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   const long long lds = k.off_stage + (long long)ch * row_bytes;
   if (lds > LDS_LIMIT) return fail(SWARM_ELIMIT, "LDS footprint %lld B exceeds %d B (N=%d, M=%d)", lds, LDS_LIMIT, k.N, k.M);
   k.obs_vec4 = (((long long)rows * k.D) % 4 == 0 && ((long long)ch * k.D) % 4 == 0) ? 1 : 0;
-  const int nb_bits = ilog2(k.N > 1 ? k.N : 2);
+  // neighbour keys carry an index in [0, 2L) in the wave kernel (unwrapped rotation index)
+  const int nb_bits = k.log2_lanes + (wave ? 1 : 0);
   const int ob_bits = ilog2(k.M > 1 ? k.M : 2);
-  k.nb_keep = ~((1u << nb_bits) - 1u);
+  k.nb_keep = nb_bits > 0 ? ~((1u << nb_bits) - 1u) : ~0u;
   k.ob_keep = ~((1u << ob_bits) - 1u);
   k.env_offset = p->env_offset;
   k.seed_lo = (unsigned)(p->seed & 0xffffffffull);
@@ -859,11 +982,12 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   k.dt = (float)p->dt;
   k.vmax = (float)p->max_speed;
   k.amax = (float)p->max_accel;
-  k.eps_speed = (float)1e-8;
   k.ds_f = (float)p->desired_spacing;
-  k.s_pair = s_threshold((float)(2.0 * p->collision_radius));
+  k.thr_pair = (float)(2.0 * p->collision_radius);
+  k.s_pair = s_threshold(k.thr_pair);
   k.s_obst = s_threshold((float)(p->collision_radius + p->obstacle_radius));
-  k.s_phys_pair = s_threshold((float)(2.0 * p->drone_contact_radius));
+  k.thr_ppair = (float)(2.0 * p->drone_contact_radius);
+  k.s_phys_pair = s_threshold(k.thr_ppair);
   k.s_phys_obst = s_threshold((float)(p->obstacle_radius + p->drone_contact_radius));
   k.ground_z = (float)p->ground_contact_height;
   k.h = (float)p->substep_dt;
@@ -877,9 +1001,9 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   k.vmax_d = p->max_speed;
   *kp = k;
   if (info) {
-    info->threads_per_block = k.threads;
+    info->threads_per_block = threads;
     info->envs_per_block = G;
-    info->lanes_per_env = k.lanes;
+    info->lanes_per_env = lanes;
     info->blocks = (int)((k.E + G - 1) / G);
     info->lds_bytes = (int)lds;
     info->neighbor_slots = neighbor_slots(k.K);
@@ -893,28 +1017,28 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
 typedef void (*kernel_fn)(const KParams, const swarm_state_t, const float*, const uint8_t*, const swarm_out_t,
                           const uint8_t*, int);
 
-template <int DYN, int KS, bool WAVE>
+template <int KIND, int DYN, int KS, bool WAVE>
 kernel_fn pick_ms(int msl) {
   switch (msl) {
-    case 0: return swarm_kernel<DYN, KS, 0, WAVE>;
-    case 5: return swarm_kernel<DYN, KS, 5, WAVE>;
-    case 9: return swarm_kernel<DYN, KS, 9, WAVE>;
-    default: return swarm_kernel<DYN, KS, 17, WAVE>;
+    case 0: return swarm_kernel<KIND, DYN, KS, 0, WAVE>;
+    case 5: return swarm_kernel<KIND, DYN, KS, 5, WAVE>;
+    case 9: return swarm_kernel<KIND, DYN, KS, 9, WAVE>;
+    default: return swarm_kernel<KIND, DYN, KS, 17, WAVE>;
   }
 }
-template <int DYN, bool WAVE>
+template <int KIND, int DYN, bool WAVE>
 kernel_fn pick_ks(int ks, int msl) {
   switch (ks) {
-    case 0: return pick_ms<DYN, 0, WAVE>(msl);
-    case 4: return pick_ms<DYN, 4, WAVE>(msl);
-    case 5: return pick_ms<DYN, 5, WAVE>(msl);
-    case 9: return pick_ms<DYN, 9, WAVE>(msl);
-    default: return pick_ms<DYN, 17, WAVE>(msl);
+    case 0: return pick_ms<KIND, DYN, 0, WAVE>(msl);
+    case 4: return pick_ms<KIND, DYN, 4, WAVE>(msl);
+    case 9: return pick_ms<KIND, DYN, 9, WAVE>(msl);
+    default: return pick_ms<KIND, DYN, 17, WAVE>(msl);
   }
 }
-kernel_fn pick(int dyn, bool wave, int ks, int msl) {
-  if (dyn == DYN_KIN) return wave ? pick_ks<DYN_KIN, true>(ks, msl) : pick_ks<DYN_KIN, false>(ks, msl);
-  return wave ? pick_ks<DYN_PHYS, true>(ks, msl) : pick_ks<DYN_PHYS, false>(ks, msl);
+template <int KIND>
+kernel_fn pick_kind(int dyn, bool wave, int ks, int msl) {
+  if (dyn == DYN_KIN) return wave ? pick_ks<KIND, DYN_KIN, true>(ks, msl) : pick_ks<KIND, DYN_KIN, false>(ks, msl);
+  return wave ? pick_ks<KIND, DYN_PHYS, true>(ks, msl) : pick_ks<KIND, DYN_PHYS, false>(ks, msl);
 }
 
 int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const float* actions, const uint8_t* amask,
@@ -936,8 +1060,9 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
       return fail(SWARM_ENULL, "out.reward/terminated/truncated/env_done required by swarm_step");
   }
   if (((uintptr_t)o->obs) % 16 != 0) kp.obs_vec4 = 0;
-  const bool wave = kp.lanes <= 64;
-  kernel_fn fn = pick(p->dynamics, wave, info.neighbor_slots, info.obstacle_slots);
+  const bool wave = (1 << kp.log2_lanes) <= 64;
+  kernel_fn fn = (mode == MODE_STEP) ? pick_kind<KIND_STEP>(p->dynamics, wave, info.neighbor_slots, info.obstacle_slots)
+                                     : pick_kind<KIND_AUX>(p->dynamics, wave, info.neighbor_slots, info.obstacle_slots);
   if (info.lds_bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        info.lds_bytes);
@@ -955,6 +1080,12 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
 extern "C" {
 
 int swarm_abi_version(void) { return SWARM_ABI_VERSION; }
+
+#ifdef SWARM_STAMPS
+int swarm_debug_stamps(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
+}
+#endif
 
 const char* swarm_last_error(void) { return g_err; }
 

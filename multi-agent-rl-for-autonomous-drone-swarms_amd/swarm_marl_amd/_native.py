@@ -108,6 +108,8 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
+    if path is None and os.environ.get("SWARM_MI355X_LIB"):
+        path = os.environ["SWARM_MI355X_LIB"]  # diagnostic builds (tools/ablate.sh)
     p = Path(path) if path is not None else LIB_PATH
     if not p.exists():
         raise NativeLibraryError(

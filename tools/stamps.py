@@ -1,0 +1,88 @@
+"""Per-phase cycle profile of the step kernel from s_memtime stamps (diagnostic build).
+
+Build:  hipcc ... -DSWARM_STAMPS -> build/stamps/libswarm_stamps.so   (tools/stamps.py build)
+Run:    SWARM_MI355X_LIB=build/stamps/libswarm_stamps.so python tools/stamps.py run [E] [N]
+"""
+import ctypes
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+LIB = ROOT / "build" / "stamps" / "libswarm_stamps.so"
+NAMES = ["load", "integrate", "pairs+obst", "topk", "reward", "reset", "writeback", "obs"]
+
+if sys.argv[1] == "build":
+    LIB.parent.mkdir(parents=True, exist_ok=True)
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+                    "-I", str(ROOT / "include"), "-DSWARM_STAMPS",
+                    str(ROOT / "multi-agent-rl-for-autonomous-drone-swarms_amd/csrc/swarm_kernel.hip"),
+                    "-o", str(LIB)], check=True)
+    sys.exit(0)
+
+os.environ["SWARM_MI355X_LIB"] = str(LIB)
+sys.path.insert(0, str(ROOT / "multi-agent-rl-for-autonomous-drone-swarms_amd"))
+import numpy as np
+import torch
+from swarm_marl_amd import VecSwarm
+from swarm_marl_amd import _native as nat
+
+e = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
+n = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+vec = VecSwarm(e, {"num_drones": n}, device="cuda:0", auto_reset=True, seed=0)
+vec.reset()
+lib = nat.load_library()
+lib.swarm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+g = torch.Generator(device="cuda:0").manual_seed(1)
+acts = [torch.rand((e, n, 3), device="cuda:0", generator=g) * 2 - 1 for _ in range(4)]
+for k in range(20):
+    vec.step(acts[k % 4])
+torch.cuda.synchronize()
+blocks = vec.launch_info.blocks
+buf = np.zeros(min(blocks, 1 << 16) * 16, np.uint64)
+lib.swarm_debug_stamps(buf.ctypes.data, buf.size)
+st = buf.reshape(-1, 16)[:, :9].astype(np.int64)
+d = np.diff(st, axis=1)
+t0 = st[:, 0].min()
+print(f"E={e} N={n} blocks={blocks}: wave lifetime cycles mean {np.mean(st[:,8]-st[:,0]):.0f} "
+      f"median {np.median(st[:,8]-st[:,0]):.0f}; kernel span {st[:,8].max()-t0} cycles; "
+      f"start spread {st[:,0].max()-t0}")
+for i, nm in enumerate(NAMES):
+    print(f"  {nm:12s} mean {d[:, i].mean():9.0f}  median {np.median(d[:, i]):9.0f}  p90 {np.percentile(d[:, i], 90):9.0f}")
+
+# ---- residency census: concurrent waves per CU from (start, end) stamps and HW_ID / XCC_ID
+hw = buf.reshape(-1, 16)[:, 9].astype(np.int64)
+xcc = buf.reshape(-1, 16)[:, 10].astype(np.int64) & 0xF
+cu = (hw >> 8) & 0xF
+sh = (hw >> 12) & 0x1
+se = (hw >> 13) & 0x7
+simd = (hw >> 4) & 0x3
+key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+best = []
+for k in np.unique(key):
+    idx = np.nonzero(key == k)[0]
+    ev = sorted([(st[i, 0], 1) for i in idx] + [(st[i, 8], -1) for i in idx])
+    c = m = 0
+    for _, dlt in ev:
+        c += dlt
+        m = max(m, c)
+    best.append((m, len(idx)))
+best = np.array(best)
+print(f"CUs seen {len(best)}; waves per CU total mean {best[:,1].mean():.1f}; "
+      f"max concurrent waves per CU: mean {best[:,0].mean():.1f} max {best[:,0].max()} min {best[:,0].min()}")
+print("simd histogram", np.bincount(simd, minlength=4))
+
+rt0 = buf.reshape(-1, 16)[:, 11].astype(np.int64)
+rt1 = buf.reshape(-1, 16)[:, 12].astype(np.int64)
+clk = (st[:, 8] - st[:, 0]) / np.maximum(rt1 - rt0, 1) * 100e6
+print(f"in-kernel clock (memtime/memrealtime): median {np.median(clk)/1e9:.2f} GHz")
+print(f"kernel span from realtime: {(rt1.max() - rt0.min())/100:.1f} us; wave life median {np.median(rt1-rt0)/100:.2f} us, "
+      f"p90 {np.percentile(rt1-rt0, 90)/100:.2f} us")
+spans = []
+for k in np.unique(key):
+    idx = np.nonzero(key == k)[0]
+    spans.append((rt1[idx].max() - rt0[idx].min()) / 100)
+print(f"per-CU span us: mean {np.mean(spans):.1f} max {np.max(spans):.1f}; first start spread {(rt0.max()-rt0.min())/100:.1f} us")
+order = np.argsort(rt0)
+print("start times (us) of block quantiles:", [(round((rt0[order[int(q*(len(order)-1))]]-rt0.min())/100, 1)) for q in (0, .25, .5, .75, 1)])
