@@ -13,8 +13,10 @@
 // Ranking vs exactness.  The reference's neighbour distance is
 //   d = sqrtf((float)(((double)(x*x) + (double)(y*y)) + (double)(z*z)))   (OpenBLAS sdot)
 // The pair loop ranks with the cheaper all-float sum s' = ((x*x)+(y*y))+(z*z), which is within
-// 2^-21 relative of the exact s.  Neighbours are kept as packed 32-bit keys (float bits of s'
-// with the low bits replaced by the neighbour index; one v_med3_u32 per slot and insert).  The
+// 2^-21 relative of the exact s (or with d~ = v_sqrt_f32(s') in the kinematic step, whose
+// formation term needs it anyway).  Neighbours are kept as packed 32-bit keys (float bits of the
+// ranking value with the low bits replaced by the neighbour index / rotation offset; one
+// v_med3_u32 per slot and insert).  The
 // K+1 survivors are re-ranked with the exact d; a lower bound on every non-survivor proves the
 // top-K exact, else an exact selection runs (rare).  Pair collisions compare the exact nearest
 // distance (all-eligible fast path) or an error-banded running minimum with exact re-check.
@@ -33,6 +35,15 @@
 
 #pragma clang fp contract(off)
 
+// Build partitioning: the kernel instantiations are compiled as parallel translation units.
+// SWARM_PART k in 0..3 holds the kernels of (KIND, DYN) = (k >> 1, k & 1); SWARM_PART 4 holds
+// the host side and the C-ABI; SWARM_PART -1 (default) is everything in one unit (tools/).
+#ifndef SWARM_PART
+#define SWARM_PART -1
+#endif
+#define SWARM_HAS_PART(k) (SWARM_PART == -1 || SWARM_PART == (k))
+#define SWARM_HAS_HOST (SWARM_PART == -1 || SWARM_PART == 4)
+
 // Diagnostic ablation switches (tools/ablate.sh builds variants; never set in the product build)
 #ifndef SWARM_ABLATE
 #define SWARM_ABLATE 0
@@ -42,6 +53,7 @@
 #define ABL_FINISH 4   // skip the exact top-K re-ranking
 #define ABL_RESET 8    // never auto-reset
 #define ABL_OBST 16    // skip the obstacle pass
+#define ABL_W64 64     // one-team waves use the generic (rolled) pair pass
 
 // Diagnostic phase timestamps (tools/stamps.py; never set in the product build)
 #ifdef SWARM_STAMPS
@@ -150,24 +162,55 @@ __device__ __forceinline__ void draw_block(const KParams& P, long long genv, uin
 }
 
 // ------------------------------------------------------------------ pair passes
-// PASS 0: kNN keys only.  PASS 1: kinematic (+ formation sum, + running min of s' over
+// PASS 0: kNN keys only.  PASS 1: kinematic (+ formation sum, + running min of d~ over
 // active pairs unless FAST).  PASS 2: physics (+ running min over real drones unless FAST).
 // FAST: every drone of the wave's teams is eligible (all active / all real, N == L): no masks,
 // pair collisions are decided from the exact nearest neighbour after the pass.
 // `self` = this drone's eligibility; ring[j].w carries drone j's.
+//
+// Wave teams: at rotation r lane t evaluates the pair (t, t+r) once for both drones.  Keys carry
+// the rotation offset (r for the own side, L-r for the mirror), a lane-independent constant; the
+// neighbour is drone (t + offset) mod L.  The mirror receives the pair value by ds_bpermute (sign
+// bit = sender eligibility).
+// Pair value space: PASS 1 (kinematic step) ranks and exchanges d~ = v_sqrt_f32(s'), monotone in
+// s' and within 2^-21 relative of the reference distance, because the formation term needs d
+// for both drones of the pair; PASS 0/2 rank by s' (no sqrt at all).  finish_keys and the banded
+// collision test take the space into account.
+template <int PASS>
+__device__ __forceinline__ float pair_value(float s) {
+  if constexpr (PASS == 1) return __builtin_amdgcn_sqrtf(s);
+  else return s;
+}
 template <int KS, int PASS, bool FAST>
-__device__ __forceinline__ void consume(uint32_t (&nk)[KS > 0 ? KS : 1], float s, uint32_t key_low, bool pr,
-                                        uint32_t keep, float ds, float& smin, float& esum) {
-  if constexpr (KS > 0) kins<KS>(nk, (__float_as_uint(s) & keep) | key_low);
-  if constexpr (PASS != 0 && (!FAST || KS == 0)) smin = fminf(smin, (FAST || pr) ? s : __builtin_inff());
+__device__ __forceinline__ uint32_t own_pair(uint32_t (&nk)[KS > 0 ? KS : 1], float s, uint32_t low, bool pr,
+                                             uint32_t keep, float ds, float& smin, float& esum) {
+  const float v = pair_value<PASS>(s);
+  if constexpr (KS > 0) kins<KS>(nk, (__float_as_uint(v) & keep) | low);
+  if constexpr (PASS != 0 && (!FAST || KS == 0)) smin = fminf(smin, (FAST || pr) ? v : __builtin_inff());
   if constexpr (PASS == 1) {
-    // formation uses d_ij widened to double in the reference; v_sqrt_f32 of s' keeps the mean
-    // within ~1e-6 relative, far inside the 1e-5 reward contract.
-    const float e = fabsf(__builtin_amdgcn_sqrtf(s) - ds);
-    esum += (FAST || pr) ? e : 0.f;
+    // formation uses d_ij widened to double in the reference; d~ keeps the mean within ~1e-6
+    // relative, far inside the 1e-5 reward contract.
+    float e = fabsf(v - ds);
+    if constexpr (!FAST) e = pr ? e : 0.f;
+    esum += e;
+  }
+  return __float_as_uint(v);
+}
+template <int KS, int PASS, bool FAST>
+__device__ __forceinline__ void mirror_pair(uint32_t (&nk)[KS > 0 ? KS : 1], uint32_t rcv, uint32_t low, bool self,
+                                            uint32_t keep_m, float ds, float& smin, float& esum) {
+  const float v = __uint_as_float(rcv & 0x7fffffffu);
+  const bool pr = FAST || (self && !(rcv >> 31));
+  if constexpr (KS > 0) kins<KS>(nk, (rcv & keep_m) | low);
+  if constexpr (PASS != 0 && (!FAST || KS == 0)) smin = fminf(smin, pr ? v : __builtin_inff());
+  if constexpr (PASS == 1) {
+    float e = fabsf(v - ds);
+    if constexpr (!FAST) e = pr ? e : 0.f;
+    esum += e;
   }
 }
 
+// General wave team (L = 2..64, G = 64/L teams per wave).
 template <int KS, int PASS, bool FAST>
 __device__ __forceinline__ void pair_pass_wave(const float4* __restrict__ ring, int L, int t, int tid, float px,
                                                float py, float pz, bool self, uint32_t keep, float ds,
@@ -175,12 +218,12 @@ __device__ __forceinline__ void pair_pass_wave(const float4* __restrict__ ring, 
   const int half = L >> 1;
   if (half == 0) return;
   const uint32_t sflag = (FAST || self) ? 0u : 0x80000000u;
+  const uint32_t keep_m = keep & 0x7fffffffu;
   const uint32_t lm4 = (uint32_t)(L - 1) << 2;
   const uint32_t tid4 = (uint32_t)tid << 2;
   const uint32_t hi4 = tid4 & ~lm4;
-  const uint32_t own0 = (uint32_t)t;        // own key index = t + r   (mod L after the pass)
-  const uint32_t mir0 = (uint32_t)(t + L);  // mirror key index = t + L - r
-  const float4* q0 = ring + t;              // ring holds drone j at j and j + L
+  const uint32_t Lu = (uint32_t)L;
+  const float4* q0 = ring + t;  // ring holds drone j at j and j + L
   // Rotations 1 .. half-1 carry a mirror, processed two at a time so that two independent
   // distance chains and two ds_bpermutes are in flight together.
   int r = 1;
@@ -191,15 +234,13 @@ __device__ __forceinline__ void pair_pass_wave(const float4* __restrict__ ring, 
     const float sb = sqsum_f(qb.x - px, qb.y - py, qb.z - pz);
     const uint32_t srca = ((tid4 - ((uint32_t)r << 2)) & lm4) | hi4;  // lane (t - r) mod L
     const uint32_t srcb = ((tid4 - ((uint32_t)(r + 1) << 2)) & lm4) | hi4;
-    const uint32_t ra = (uint32_t)__builtin_amdgcn_ds_bpermute((int)srca, (int)(__float_as_uint(sa) | sflag));
-    const uint32_t rb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)srcb, (int)(__float_as_uint(sb) | sflag));
     float esum = 0.f;
-    consume<KS, PASS, FAST>(nk, sa, own0 + (uint32_t)r, self && (qa.w != 0.f), keep, ds, smin, esum);
-    consume<KS, PASS, FAST>(nk, sb, own0 + (uint32_t)(r + 1), self && (qb.w != 0.f), keep, ds, smin, esum);
-    consume<KS, PASS, FAST>(nk, __uint_as_float(ra & 0x7fffffffu), mir0 - (uint32_t)r, self && !(ra >> 31), keep,
-                            ds, smin, esum);
-    consume<KS, PASS, FAST>(nk, __uint_as_float(rb & 0x7fffffffu), mir0 - (uint32_t)(r + 1), self && !(rb >> 31),
-                            keep, ds, smin, esum);
+    const uint32_t va = own_pair<KS, PASS, FAST>(nk, sa, (uint32_t)r, self && (qa.w != 0.f), keep, ds, smin, esum);
+    const uint32_t vb = own_pair<KS, PASS, FAST>(nk, sb, (uint32_t)(r + 1), self && (qb.w != 0.f), keep, ds, smin, esum);
+    const uint32_t ra = (uint32_t)__builtin_amdgcn_ds_bpermute((int)srca, (int)(va | sflag));
+    const uint32_t rb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)srcb, (int)(vb | sflag));
+    mirror_pair<KS, PASS, FAST>(nk, ra, Lu - (uint32_t)r, self, keep_m, ds, smin, esum);
+    mirror_pair<KS, PASS, FAST>(nk, rb, Lu - (uint32_t)(r + 1), self, keep_m, ds, smin, esum);
     if constexpr (PASS == 1) fsum += (double)esum;
   }
   float esum = 0.f;
@@ -207,15 +248,54 @@ __device__ __forceinline__ void pair_pass_wave(const float4* __restrict__ ring, 
     const float4 qa = q0[r];
     const float sa = sqsum_f(qa.x - px, qa.y - py, qa.z - pz);
     const uint32_t srca = ((tid4 - ((uint32_t)r << 2)) & lm4) | hi4;
-    const uint32_t ra = (uint32_t)__builtin_amdgcn_ds_bpermute((int)srca, (int)(__float_as_uint(sa) | sflag));
-    consume<KS, PASS, FAST>(nk, sa, own0 + (uint32_t)r, self && (qa.w != 0.f), keep, ds, smin, esum);
-    consume<KS, PASS, FAST>(nk, __uint_as_float(ra & 0x7fffffffu), mir0 - (uint32_t)r, self && !(ra >> 31), keep,
-                            ds, smin, esum);
+    const uint32_t va = own_pair<KS, PASS, FAST>(nk, sa, (uint32_t)r, self && (qa.w != 0.f), keep, ds, smin, esum);
+    const uint32_t ra = (uint32_t)__builtin_amdgcn_ds_bpermute((int)srca, (int)(va | sflag));
+    mirror_pair<KS, PASS, FAST>(nk, ra, Lu - (uint32_t)r, self, keep_m, ds, smin, esum);
   }
   // r = L/2 pairs t with t+L/2 from both sides: own evaluation only
   const float4 qh = q0[half];
   const float sh = sqsum_f(qh.x - px, qh.y - py, qh.z - pz);
-  consume<KS, PASS, FAST>(nk, sh, own0 + (uint32_t)half, self && (qh.w != 0.f), keep, ds, smin, esum);
+  own_pair<KS, PASS, FAST>(nk, sh, (uint32_t)half, self && (qh.w != 0.f), keep, ds, smin, esum);
+  if constexpr (PASS == 1) fsum += (double)esum;
+}
+
+// One team per wave (L = 64): fully unrolled, every LDS / ds_bpermute address is the lane's
+// base plus an immediate offset (ds_bpermute takes the source lane modulo 64).
+template <int KS, int PASS, bool FAST>
+__device__ __forceinline__ void pair_pass_w64(const float4* __restrict__ ring, int t, float px, float py, float pz,
+                                              bool self, uint32_t keep, float ds, uint32_t (&nk)[KS > 0 ? KS : 1],
+                                              float& smin, double& fsum) {
+  const uint32_t sflag = (FAST || self) ? 0u : 0x80000000u;
+  const uint32_t keep_m = keep & 0x7fffffffu;
+  const uint32_t t4 = (uint32_t)t << 2;
+  const float4* q0 = ring + t;
+#pragma unroll
+  for (int r = 1; r < 31; r += 2) {
+    const float4 qa = q0[r];
+    const float4 qb = q0[r + 1];
+    const float sa = sqsum_f(qa.x - px, qa.y - py, qa.z - pz);
+    const float sb = sqsum_f(qb.x - px, qb.y - py, qb.z - pz);
+    float esum = 0.f;
+    const uint32_t va = own_pair<KS, PASS, FAST>(nk, sa, (uint32_t)r, self && (qa.w != 0.f), keep, ds, smin, esum);
+    const uint32_t vb = own_pair<KS, PASS, FAST>(nk, sb, (uint32_t)(r + 1), self && (qb.w != 0.f), keep, ds, smin, esum);
+    const uint32_t ra = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t4 + (uint32_t)(256 - 4 * r)), (int)(va | sflag));
+    const uint32_t rb =
+        (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t4 + (uint32_t)(256 - 4 * (r + 1))), (int)(vb | sflag));
+    mirror_pair<KS, PASS, FAST>(nk, ra, (uint32_t)(64 - r), self, keep_m, ds, smin, esum);
+    mirror_pair<KS, PASS, FAST>(nk, rb, (uint32_t)(64 - r - 1), self, keep_m, ds, smin, esum);
+    if constexpr (PASS == 1) fsum += (double)esum;
+  }
+  float esum = 0.f;
+  {  // r = 31: last rotation with a mirror
+    const float4 qa = q0[31];
+    const float sa = sqsum_f(qa.x - px, qa.y - py, qa.z - pz);
+    const uint32_t va = own_pair<KS, PASS, FAST>(nk, sa, 31u, self && (qa.w != 0.f), keep, ds, smin, esum);
+    const uint32_t ra = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t4 + (uint32_t)(256 - 4 * 31)), (int)(va | sflag));
+    mirror_pair<KS, PASS, FAST>(nk, ra, 33u, self, keep_m, ds, smin, esum);
+  }
+  const float4 qh = q0[32];
+  const float sh = sqsum_f(qh.x - px, qh.y - py, qh.z - pz);
+  own_pair<KS, PASS, FAST>(nk, sh, 32u, self && (qh.w != 0.f), keep, ds, smin, esum);
   if constexpr (PASS == 1) fsum += (double)esum;
 }
 
@@ -226,13 +306,13 @@ __device__ __forceinline__ void pair_pass_block(const float4* __restrict__ pos4,
 #pragma unroll 4
   for (int j = 0; j < N; ++j) {
     const float4 q = pos4[j];
-    const float s = sqsum_f(q.x - px, q.y - py, q.z - pz);
+    const float v = pair_value<PASS>(sqsum_f(q.x - px, q.y - py, q.z - pz));
     const bool other = j != t;
-    if constexpr (KS > 0) kins<KS>(nk, other ? ((__float_as_uint(s) & keep) | (uint32_t)j) : KEY_EMPTY);
+    if constexpr (KS > 0) kins<KS>(nk, other ? ((__float_as_uint(v) & keep) | (uint32_t)j) : KEY_EMPTY);
     const bool pr = self && (q.w != 0.f) && other;
-    if constexpr (PASS != 0) smin = fminf(smin, pr ? s : __builtin_inff());
+    if constexpr (PASS != 0) smin = fminf(smin, pr ? v : __builtin_inff());
     if constexpr (PASS == 1) {
-      const float e = fabsf(__builtin_amdgcn_sqrtf(s) - ds);
+      const float e = fabsf(v - ds);
       fsum += (double)(pr ? e : 0.f);
     }
   }
@@ -252,12 +332,13 @@ __device__ __forceinline__ void obstacle_pass(const float4* __restrict__ obst4, 
 
 // Re-rank the S surviving keys by exact distance (the reference sorts by the float distance;
 // ties by index).  Returns false when an entry outside the survivors could still precede the
-// K-th winner — the caller then runs exact_select.  APPROX: keys hold s' (pairs) rather than the
-// exact value (obstacles), so the non-survivor bound is widened by FAST_LO.
+// K-th winner — the caller then runs exact_select.  APPROX: keys hold s' or d~ (pairs; `dkey`
+// selects d~) rather than the exact squared value (obstacles), so the non-survivor bound is
+// widened by FAST_LO.
 template <int S, bool AXIS, bool APPROX>
 __device__ __forceinline__ bool finish_keys(const uint32_t (&k)[S], const float4* __restrict__ pts, int count,
-                                            int imod, int K, uint32_t keep, float px, float py, float pz,
-                                            float (&wd)[S], int (&wj)[S]) {
+                                            int ibase, int imod, int K, uint32_t keep, bool dkey, float px, float py,
+                                            float pz, float (&wd)[S], int (&wj)[S]) {
   const uint32_t imask = ~keep;
   // The keys are already ordered by the (truncated) ranking value; the exact order can differ
   // only where two survivors lie within the truncation/error band of each other (near-tie,
@@ -272,7 +353,7 @@ __device__ __forceinline__ bool finish_keys(const uint32_t (&k)[S], const float4
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const uint32_t key = k[s];
-    const int j = (int)(key & imask) & imod;
+    const int j = ((int)(key & imask) + ibase) & imod;
     const bool valid = (key != KEY_EMPTY) && (j < count) && (s < need);
     float d = __builtin_inff();
     if (valid) {
@@ -296,55 +377,71 @@ __device__ __forceinline__ bool finish_keys(const uint32_t (&k)[S], const float4
     }
   }
   const uint32_t last = k[S - 1];
-  if (last == KEY_EMPTY || (int)((last & imask) & imod) >= count) return true;
+  if (last == KEY_EMPTY || ((((int)(last & imask) + ibase) & imod) >= count)) return true;
   if (K <= 0) return true;
   const float base = __uint_as_float(last & keep);
-  const float dlb = sqrt_rn(APPROX ? base * FAST_LO : base);
+  const float dlb = APPROX ? (dkey ? base * FAST_LO : sqrt_rn(base * FAST_LO)) : sqrt_rn(base);
   return dlb > wd[K - 1];
 }
 
-// Exact (distance, index) selection of the K nearest of `count` points (rare fallback).
-template <int S, bool AXIS>
-__device__ __forceinline__ void exact_select(const float4* __restrict__ pts, int count, int self, int K, float px,
-                                             float py, float pz, float (&wd)[S], int (&wj)[S]) {
-  float pd = -1.f;
-  int pj = -1;
+// arr[idx] of a register array without dynamic indexing (which would move it to scratch)
+template <int S>
+__device__ __forceinline__ float reg_at(const float (&arr)[S], int idx) {
+  float v = arr[0];
 #pragma unroll
-  for (int k = 0; k < S; ++k) {
-    float bd = __builtin_inff();
-    int bj = 0x7fffffff;
-    if (k < K) {
-      for (int j = 0; j < count; ++j) {
-        if (j == self) continue;
-        const float4 q = pts[j];
-        const float d = AXIS ? sqrt_rn(sqsum_f(q.x - px, q.y - py, q.z - pz))
-                             : sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
-        const bool gt = (d > pd) || (d == pd && j > pj);
-        const bool lt = (d < bd) || (d == bd && j < bj);
-        if (gt && lt) { bd = d; bj = j; }
+  for (int u = 1; u < S; ++u) v = (u == idx) ? arr[u] : v;
+  return v;
+}
+
+// Exact (distance, index) selection of the K nearest of `count` points (rare fallback, taken when
+// finish_keys cannot prove its top-K).  `dmax` bounds the K-th exact distance from above (the
+// K-th of the re-ranked survivors), so only points whose f32 squared sum lies within dmax^2 (plus
+// the f32 error band) can belong to the answer: a cheap scan filters, and the exact distance is
+// evaluated only for those few.
+template <int S, bool AXIS>
+__device__ __forceinline__ void exact_select(const float4* __restrict__ pts, int count, int self, int K, float dmax,
+                                             float px, float py, float pz, float (&wd)[S], int (&wj)[S]) {
+#pragma unroll
+  for (int u = 0; u < S; ++u) { wd[u] = __builtin_inff(); wj[u] = 0x7fffffff; }
+  const float s_cut = (dmax * dmax) * FAST_HI;
+  for (int j = 0; j < count; ++j) {
+    const float4 q = pts[j];
+    const float sq = sqsum_f(q.x - px, q.y - py, q.z - pz);
+    if (j != self && sq <= s_cut) {
+      float cd = AXIS ? sqrt_rn(sq) : sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
+      int cj = j;
+#pragma unroll
+      for (int u = 0; u < S; ++u) {  // insertion by exchange: the largest falls off slot K-1
+        if (u < K) {
+          const bool lt = (cd < wd[u]) || (cd == wd[u] && cj < wj[u]);
+          const float td = wd[u];
+          const int tj = wj[u];
+          wd[u] = lt ? cd : td; wj[u] = lt ? cj : tj;
+          cd = lt ? td : cd; cj = lt ? tj : cj;
+        }
       }
     }
-    wd[k] = bd;
-    wj[k] = bj;
-    pd = bd;
-    pj = bj;
   }
 }
 
-// exact "any eligible pair within s_thr" (fallback of the banded running minimum)
+// exact "any eligible pair within s_thr" (fallback of the banded running minimum); the f32 sum
+// filters, the sdot-exact sum decides
 __device__ __forceinline__ bool exact_pair_collision(const float4* __restrict__ pts, int count, int self,
                                                      float px, float py, float pz, float s_thr) {
   bool c = false;
+  const float s_cut = s_thr * FAST_HI;
   for (int j = 0; j < count; ++j) {
     const float4 q = pts[j];
-    if (j != self && q.w != 0.f) c = c || (sqsum_1d(q.x - px, q.y - py, q.z - pz) <= s_thr);
+    if (j != self && q.w != 0.f && sqsum_f(q.x - px, q.y - py, q.z - pz) <= s_cut)
+      c = c || (sqsum_1d(q.x - px, q.y - py, q.z - pz) <= s_thr);
   }
   return c;
 }
 
 // ------------------------------------------------------------------ the kernel
-template <int KIND, int DYN, int KS, int MSL, bool WAVE>
-__global__ void __launch_bounds__(WAVE ? 64 : 1024)
+// LM (lane mode): 0 = BLOCK (L > 64), 1 = WAVE with 64/L teams, 2 = WAVE with one team (L == 64)
+template <int KIND, int DYN, int KS, int MSL, int LM>
+__global__ void __launch_bounds__(LM != 0 ? 64 : 1024)
 swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ actions,
              const uint8_t* __restrict__ amask, const swarm_out_t O,
              const uint8_t* __restrict__ env_mask, int mode_arg) {
@@ -355,11 +452,13 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
 #ifdef SWARM_STAMPS
   if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) g_stamps[blockIdx.x * 16 + 11] = __builtin_amdgcn_s_memrealtime();
 #endif
+  constexpr bool WAVE = LM != 0;
+  constexpr bool W64 = LM == 2;
   const int tid = threadIdx.x;
-  const int L = 1 << P.log2_lanes;
-  const int team = tid >> P.log2_lanes;
-  const int t = tid & (L - 1);
-  const int G = P.envs_per_block;
+  const int L = W64 ? 64 : 1 << P.log2_lanes;
+  const int team = W64 ? 0 : tid >> P.log2_lanes;
+  const int t = W64 ? tid : tid & (L - 1);
+  const int G = W64 ? 1 : P.envs_per_block;
   const int N = P.N, M = P.M, D = P.D, K = P.K, Ms = P.Ms;
   const long long env0 = (long long)blockIdx.x * G;
   const long long env = env0 + team;
@@ -369,7 +468,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   float4* obst4 = reinterpret_cast<float4*>(smem + P.off_obst) + team * P.obst_stride;
   float* stage = reinterpret_cast<float*>(smem + P.off_stage);
   uint64_t team_bits = 0;
-  if constexpr (WAVE) team_bits = (L == 64) ? ~0ull : (((1ull << L) - 1ull) << (team * L));
+  if constexpr (WAVE) team_bits = (W64 || L == 64) ? ~0ull : (((1ull << L) - 1ull) << (team * L));
 
   // envs this call writes: every env (step) or the masked ones (reset / observe)
   bool sel = env_ok;
@@ -529,7 +628,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
 #pragma unroll
   for (int s = 0; s < OW; ++s) ok[s] = KEY_EMPTY;
   bool ocoll = false;
-  float smin = __builtin_inff();  // running min of s' over eligible pairs (banded)
+  float smin = __builtin_inff();  // running min of the pair value over eligible pairs (banded)
   double fsum = 0.0;
   const bool pass_env = (mode == MODE_STEP) ? env_ok : sel;
   // all-eligible fast path: wave-uniform, needs the nearest neighbour (KS > 0) and no padding
@@ -539,8 +638,15 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     if (mode == MODE_STEP) {
       constexpr int PASS = (DYN == DYN_KIN) ? 1 : 2;
       if constexpr (WAVE) {
-        if (fast) pair_pass_wave<KS, PASS, true>(ring, L, t, tid, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
-        else pair_pass_wave<KS, PASS, false>(ring, L, t, tid, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
+        if constexpr (W64 && !(SWARM_ABLATE & ABL_W64)) {
+          if (fast) pair_pass_w64<KS, PASS, true>(ring, t, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
+          else pair_pass_w64<KS, PASS, false>(ring, t, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
+        } else {
+          if (fast)
+            pair_pass_wave<KS, PASS, true>(ring, L, t, tid, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
+          else
+            pair_pass_wave<KS, PASS, false>(ring, L, t, tid, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
+        }
       } else {
         pair_pass_block<KS, PASS>(ring, N, t, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
       }
@@ -548,8 +654,12 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       else if constexpr (DYN == DYN_KIN) obstacle_pass<MSL, true>(obst4, M, px, py, pz, act, P.s_obst, P.ob_keep, ok, ocoll);
       else obstacle_pass<MSL, true>(obst4, M, px, py, pz, true, P.s_phys_obst, P.ob_keep, ok, ocoll);
     } else {
-      if constexpr (WAVE) pair_pass_wave<KS, 0, true>(ring, L, t, tid, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
-      else pair_pass_block<KS, 0>(ring, N, t, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
+      if constexpr (WAVE) {
+        if constexpr (W64 && !(SWARM_ABLATE & ABL_W64)) pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
+        else pair_pass_wave<KS, 0, true>(ring, L, t, tid, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
+      } else {
+        pair_pass_block<KS, 0>(ring, N, t, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
+      }
       obstacle_pass<MSL, false>(obst4, M, px, py, pz, false, 0.f, P.ob_keep, ok, ocoll);
     }
   }
@@ -565,20 +675,21 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   const int imod = WAVE ? (L - 1) : 0x7fffffff;
   const int Kq = (fast && K < 1) ? 1 : K;  // the fast collision test needs the nearest
   const int Mse = Ms < M ? Ms : M;
-  auto select_topk = [&](bool run) {
+  auto select_topk = [&](bool run, bool dkey) {
     bool slow_nb = false, slow_ob = false;
     if (run && !(SWARM_ABLATE & ABL_FINISH)) {
-      if constexpr (KS > 0) slow_nb = !finish_keys<KS, false, true>(nk, ring, N, imod, Kq, P.nb_keep, px, py, pz, wd, wj);
-      if constexpr (MSL > 0) slow_ob = !finish_keys<MSL, true, false>(ok, obst4, M, 0x7fffffff, Mse, P.ob_keep, px, py, pz, od, oj);
+      if constexpr (KS > 0) slow_nb = !finish_keys<KS, false, true>(nk, ring, N, WAVE ? t : 0, imod, Kq, P.nb_keep, dkey, px, py, pz, wd, wj);
+      if constexpr (MSL > 0) slow_ob = !finish_keys<MSL, true, false>(ok, obst4, M, 0, 0x7fffffff, Mse, P.ob_keep, false, px, py, pz, od, oj);
     }
     if constexpr (KS > 0) {
-      if (slow_nb) exact_select<NW, false>(ring, N, t, Kq, px, py, pz, wd, wj);
+      if (slow_nb) exact_select<NW, false>(ring, N, t, Kq, reg_at(wd, Kq - 1), px, py, pz, wd, wj);
     }
     if constexpr (MSL > 0) {
-      if (slow_ob) exact_select<OW, true>(obst4, M, -1, Mse, px, py, pz, od, oj);
+      if (slow_ob) exact_select<OW, true>(obst4, M, -1, Mse, reg_at(od, Mse - 1), px, py, pz, od, oj);
     }
   };
-  select_topk(is_agent && pass_env);
+  // the step's kinematic pass ranks by d~, every other pass by s'
+  select_topk(is_agent && pass_env, KIND == KIND_STEP && DYN == DYN_KIN);
   STAMP(4);
 
   // ---- rewards / terminations (step)
@@ -591,12 +702,15 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     if (is_agent) {
       // pair collision: exact nearest (fast) or banded running minimum with exact re-check
       const float s_exact_thr = (DYN == DYN_KIN) ? P.s_pair : P.s_phys_pair;
+      const float d_thr = (DYN == DYN_KIN) ? P.thr_pair : P.thr_ppair;
       bool pcoll;
       if (fast) {
-        pcoll = wd[0] <= ((DYN == DYN_KIN) ? P.thr_pair : P.thr_ppair);
+        pcoll = wd[0] <= d_thr;
       } else {
-        pcoll = smin <= s_exact_thr * FAST_LO;
-        if (!pcoll && smin <= s_exact_thr * FAST_HI && elig)
+        // smin holds d~ (kinematic) or s' (physics): certain below the band, exact inside it
+        const float band_thr = (DYN == DYN_KIN) ? d_thr : s_exact_thr;
+        pcoll = smin <= band_thr * FAST_LO;
+        if (!pcoll && smin <= band_thr * FAST_HI && elig)
           pcoll = exact_pair_collision(ring, N, t, px, py, pz, s_exact_thr);
       }
       if constexpr (DYN == DYN_KIN) {
@@ -704,11 +818,13 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         bool c2 = false;
         float s2 = 0.f;
         double f2 = 0.0;
-        if constexpr (WAVE) pair_pass_wave<KS, 0, true>(ring, L, t, tid, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
-        else pair_pass_block<KS, 0>(ring, N, t, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
+        if constexpr (WAVE) {
+          if constexpr (W64 && !(SWARM_ABLATE & ABL_W64)) pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
+          else pair_pass_wave<KS, 0, true>(ring, L, t, tid, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
+        } else pair_pass_block<KS, 0>(ring, N, t, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
         obstacle_pass<MSL, false>(obst4, M, px, py, pz, false, 0.f, P.ob_keep, ok, c2);
       }
-      select_topk(do_reset && is_agent);
+      select_topk(do_reset && is_agent, false);
     }
   } else if (sel && is_agent) {
     dist_out = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
@@ -861,6 +977,59 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
 }
 
 // ------------------------------------------------------------------ host side
+typedef void (*kernel_fn)(const KParams, const swarm_state_t, const float*, const uint8_t*, const swarm_out_t,
+                          const uint8_t*, int);
+
+template <int KIND, int DYN, int KS, int LM>
+kernel_fn pick_ms(int msl) {
+  switch (msl) {
+    case 0: return swarm_kernel<KIND, DYN, KS, 0, LM>;
+    case 5: return swarm_kernel<KIND, DYN, KS, 5, LM>;
+    case 9: return swarm_kernel<KIND, DYN, KS, 9, LM>;
+    default: return swarm_kernel<KIND, DYN, KS, 17, LM>;
+  }
+}
+template <int KIND, int DYN, int LM>
+kernel_fn pick_ks(int ks, int msl) {
+  switch (ks) {
+    case 0: return pick_ms<KIND, DYN, 0, LM>(msl);
+    case 4: return pick_ms<KIND, DYN, 4, LM>(msl);
+    case 9: return pick_ms<KIND, DYN, 9, LM>(msl);
+    default: return pick_ms<KIND, DYN, 17, LM>(msl);
+  }
+}
+template <int KIND, int DYN>
+void* pick_lm(int lm, int ks, int msl) {
+  switch (lm) {
+    case 0: return reinterpret_cast<void*>(pick_ks<KIND, DYN, 0>(ks, msl));
+    case 1: return reinterpret_cast<void*>(pick_ks<KIND, DYN, 1>(ks, msl));
+    default: return reinterpret_cast<void*>(pick_ks<KIND, DYN, 2>(ks, msl));
+  }
+}
+
+}  // namespace
+
+// kernel tables, one per translation unit (SWARM_PART); returns the host stub of the kernel
+#define SWARM_PICK_DECL(k) __attribute__((visibility("hidden"))) void* swarm_pick_##k(int lm, int ks, int msl)
+SWARM_PICK_DECL(0);
+SWARM_PICK_DECL(1);
+SWARM_PICK_DECL(2);
+SWARM_PICK_DECL(3);
+#if SWARM_HAS_PART(0)
+SWARM_PICK_DECL(0) { return pick_lm<KIND_STEP, DYN_KIN>(lm, ks, msl); }
+#endif
+#if SWARM_HAS_PART(1)
+SWARM_PICK_DECL(1) { return pick_lm<KIND_STEP, DYN_PHYS>(lm, ks, msl); }
+#endif
+#if SWARM_HAS_PART(2)
+SWARM_PICK_DECL(2) { return pick_lm<KIND_AUX, DYN_KIN>(lm, ks, msl); }
+#endif
+#if SWARM_HAS_PART(3)
+SWARM_PICK_DECL(3) { return pick_lm<KIND_AUX, DYN_PHYS>(lm, ks, msl); }
+#endif
+
+#if SWARM_HAS_HOST
+namespace {
 thread_local char g_err[512] = "";
 
 int fail(int code, const char* fmt, ...) {
@@ -968,8 +1137,8 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   const long long lds = k.off_stage + (long long)ch * row_bytes;
   if (lds > LDS_LIMIT) return fail(SWARM_ELIMIT, "LDS footprint %lld B exceeds %d B (N=%d, M=%d)", lds, LDS_LIMIT, k.N, k.M);
   k.obs_vec4 = (((long long)rows * k.D) % 4 == 0 && ((long long)ch * k.D) % 4 == 0) ? 1 : 0;
-  // neighbour keys carry an index in [0, 2L) in the wave kernel (unwrapped rotation index)
-  const int nb_bits = k.log2_lanes + (wave ? 1 : 0);
+  // neighbour keys carry the drone index (block) or the rotation offset in [1, L) (wave)
+  const int nb_bits = k.log2_lanes;
   const int ob_bits = ilog2(k.M > 1 ? k.M : 2);
   k.nb_keep = nb_bits > 0 ? ~((1u << nb_bits) - 1u) : ~0u;
   k.ob_keep = ~((1u << ob_bits) - 1u);
@@ -1014,33 +1183,6 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   return SWARM_OK;
 }
 
-typedef void (*kernel_fn)(const KParams, const swarm_state_t, const float*, const uint8_t*, const swarm_out_t,
-                          const uint8_t*, int);
-
-template <int KIND, int DYN, int KS, bool WAVE>
-kernel_fn pick_ms(int msl) {
-  switch (msl) {
-    case 0: return swarm_kernel<KIND, DYN, KS, 0, WAVE>;
-    case 5: return swarm_kernel<KIND, DYN, KS, 5, WAVE>;
-    case 9: return swarm_kernel<KIND, DYN, KS, 9, WAVE>;
-    default: return swarm_kernel<KIND, DYN, KS, 17, WAVE>;
-  }
-}
-template <int KIND, int DYN, bool WAVE>
-kernel_fn pick_ks(int ks, int msl) {
-  switch (ks) {
-    case 0: return pick_ms<KIND, DYN, 0, WAVE>(msl);
-    case 4: return pick_ms<KIND, DYN, 4, WAVE>(msl);
-    case 9: return pick_ms<KIND, DYN, 9, WAVE>(msl);
-    default: return pick_ms<KIND, DYN, 17, WAVE>(msl);
-  }
-}
-template <int KIND>
-kernel_fn pick_kind(int dyn, bool wave, int ks, int msl) {
-  if (dyn == DYN_KIN) return wave ? pick_ks<KIND, DYN_KIN, true>(ks, msl) : pick_ks<KIND, DYN_KIN, false>(ks, msl);
-  return wave ? pick_ks<KIND, DYN_PHYS, true>(ks, msl) : pick_ks<KIND, DYN_PHYS, false>(ks, msl);
-}
-
 int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const float* actions, const uint8_t* amask,
            const uint8_t* env_mask, const swarm_out_t* o, void* stream) {
   KParams kp;
@@ -1060,9 +1202,13 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
       return fail(SWARM_ENULL, "out.reward/terminated/truncated/env_done required by swarm_step");
   }
   if (((uintptr_t)o->obs) % 16 != 0) kp.obs_vec4 = 0;
-  const bool wave = (1 << kp.log2_lanes) <= 64;
-  kernel_fn fn = (mode == MODE_STEP) ? pick_kind<KIND_STEP>(p->dynamics, wave, info.neighbor_slots, info.obstacle_slots)
-                                     : pick_kind<KIND_AUX>(p->dynamics, wave, info.neighbor_slots, info.obstacle_slots);
+  const int lanes = 1 << kp.log2_lanes;
+  const int lm = lanes > 64 ? 0 : (lanes == 64 ? 2 : 1);
+  const int ks = info.neighbor_slots, msl = info.obstacle_slots;
+  const bool kin = p->dynamics == DYN_KIN;
+  void* fnp = (mode == MODE_STEP) ? (kin ? swarm_pick_0(lm, ks, msl) : swarm_pick_1(lm, ks, msl))
+                                  : (kin ? swarm_pick_2(lm, ks, msl) : swarm_pick_3(lm, ks, msl));
+  kernel_fn fn = reinterpret_cast<kernel_fn>(fnp);
   if (info.lds_bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        info.lds_bytes);
@@ -1152,3 +1298,4 @@ int swarm_observe(const swarm_params_t* p, const swarm_state_t* s, const uint8_t
 }
 
 }  // extern "C"
+#endif  // SWARM_HAS_HOST

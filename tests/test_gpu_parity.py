@@ -168,3 +168,37 @@ def test_observe_masked(dev):
     torch.cuda.synchronize()
     assert np.array_equal(vec.obs.cpu().numpy(), so.observe(cfg, st2["pos"], st2["vel"],
                                                             st2["goal"], st2["obst"]))
+
+
+@pytest.mark.parametrize("n,k,ms,m", [(64, 3, 4, 8), (27, 3, 4, 8), (16, 8, 6, 8), (100, 5, 4, 12),
+                                      (64, 16, 16, 20), (8, 4, 4, 6)])
+def test_tie_heavy_lattice(dev, n, k, ms, m):
+    """Drones on an integer lattice, obstacles on a symmetric sub-lattice: exact distance ties
+    everywhere, which forces the exact top-K fallback (banded scan) and (distance, index)
+    tie-breaking for neighbours and obstacles alike."""
+    from oracle import swarm_oracle as so
+    raw = dict(num_drones=n, neighbor_k=k, sensed_obstacles=ms, num_obstacles=m, max_steps=50,
+               collision_radius=0.1)
+    cfg = oracle_cfg(raw)
+    spacings = [1.0, 0.5, 2.0, 1.5, 0.75, 1.25]
+    e = len(spacings)
+    side = int(np.ceil(n ** (1.0 / 3.0) - 1e-9))
+    grid = np.stack(np.meshgrid(*[np.arange(side)] * 3, indexing="ij"), -1).reshape(-1, 3)[:n]
+    pos = np.stack([(grid - (side - 1) / 2.0) * sp for sp in spacings]).astype(np.float32)
+    ogrid = np.stack(np.meshgrid(*[np.arange(3)] * 3, indexing="ij"), -1).reshape(-1, 3)[:m]
+    obst = np.stack([(ogrid - 1.0) * sp * 2.0 + 0.5 * sp for sp in spacings]).astype(np.float32)
+    goal = np.tile(np.array([7.25, -6.5, 3.75], np.float32), (e, 1))
+    active = np.ones((e, n), bool)
+    active[-1, ::3] = False  # one env on the masked (non-fast) path
+    st = dict(pos=pos, vel=np.zeros_like(pos), goal=goal, obst=obst, active=active,
+              step=np.zeros(e, np.int32), episode=np.zeros(e, np.uint32),
+              damping=np.zeros((e, n), np.float32))
+    vec = _vec(dev, raw, e, auto_reset=False, seed=2)
+    vec.set_state(pos=pos, vel=st["vel"], goal=goal, obstacles=obst, active=active,
+                  step_count=st["step"])
+    for t in range(2):
+        a = np.zeros((e, n, 3), np.float32)
+        vec.step(torch.as_tensor(a).to(dev))
+        torch.cuda.synchronize()
+        st, out = so.step(cfg, st, a, None, auto_reset=False, seed=2, exact_formation=True)
+        _compare_step(vec, out, st, f"lattice N={n} K={k} Ms={ms} M={m} t={t}")

@@ -10,7 +10,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-LIB = ROOT / "build" / "stamps" / "libswarm_stamps.so"
+LIB = Path(os.environ.get("SWARM_STAMPS_LIB", ROOT / "build" / "stamps" / "libswarm_stamps.so"))
 NAMES = ["load", "integrate", "pairs+obst", "topk", "reward", "reset", "writeback", "obs"]
 
 if sys.argv[1] == "build":
@@ -43,6 +43,10 @@ blocks = vec.launch_info.blocks
 buf = np.zeros(min(blocks, 1 << 16) * 16, np.uint64)
 lib.swarm_debug_stamps(buf.ctypes.data, buf.size)
 st = buf.reshape(-1, 16)[:, :9].astype(np.int64)
+dump = os.environ.get("SWARM_STAMPS_DUMP")
+if dump:
+    np.savez_compressed(dump, stamps=buf.reshape(-1, 16), env_done=vec.env_done.cpu().numpy(),
+                        active=vec.active.cpu().numpy())
 d = np.diff(st, axis=1)
 t0 = st[:, 0].min()
 print(f"E={e} N={n} blocks={blocks}: wave lifetime cycles mean {np.mean(st[:,8]-st[:,0]):.0f} "
@@ -86,3 +90,10 @@ for k in np.unique(key):
 print(f"per-CU span us: mean {np.mean(spans):.1f} max {np.max(spans):.1f}; first start spread {(rt0.max()-rt0.min())/100:.1f} us")
 order = np.argsort(rt0)
 print("start times (us) of block quantiles:", [(round((rt0[order[int(q*(len(order)-1))]]-rt0.min())/100, 1)) for q in (0, .25, .5, .75, 1)])
+
+life = (rt1 - rt0) / 100
+o = np.argsort(-life)[:12]
+print("longest waves: block, start_us, life_us, phase cycles [load integ pairs topk reward reset wb obs]")
+for i in o:
+    print(f"  {i:5d} {(rt0[i]-rt0.min())/100:7.1f} {life[i]:7.1f} {d[i].tolist()}")
+print("life quantiles us:", np.percentile(life, [50, 90, 99, 99.9, 100]).round(1).tolist())
