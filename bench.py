@@ -174,7 +174,8 @@ def main():
                          "traffic": pmc_traffic(wl),
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "kernel_ms_mean": kern_ms, "kernel_ms_mean_max_rank": kern_ms_max,
-                         "kernel": "swarm_kernel<0,4,4>"},
+                         "kernel": vec.kernel_name(),
+                         "timing": "HIP events on the launch stream around each step"},
             "env_done_fraction_last_step": done_frac,
         }
         if not args.no_cpu_baseline and world == 1:

@@ -214,6 +214,15 @@ class VecSwarm:
         d["num_drones"] = self.num_drones
         return d
 
+    def kernel_name(self) -> str:
+        """Template instantiation the step launches: swarm_kernel<KIND, DYN, KS, MSL, LM>
+        (KIND 0 = step; LM lane mode 0 block / 1 multi-team wave / 2 one team per wave)."""
+        li = self.launch_info
+        lanes = int(li.lanes_per_env)
+        lm = 0 if lanes > 64 else (2 if lanes == 64 else 1)
+        return (f"swarm_kernel<0, {int(self.params.dynamics)}, {int(li.neighbor_slots)}, "
+                f"{int(li.obstacle_slots)}, {lm}>")
+
     def algorithmic_bytes_per_step(self) -> int:
         """HBM bytes one step must move: per agent action 12 + pos/vel r/w 48 +
         active r/w 2 + obs 4D + reward 4 + terminated/truncated 2; per env goal 12 + obstacles

@@ -1,0 +1,135 @@
+"""CPU: the C-ABI library (libswarm_mi355x.so) loads, exports exactly what include/swarm_mi355x.h
+declares, and validates its arguments.  No kernel is launched: every call here either returns
+before touching the GPU (validation, zero envs) or is a pure host query.
+"""
+from __future__ import annotations
+
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "swarm_mi355x.h"
+
+
+@pytest.fixture(scope="module")
+def nat():
+    from swarm_marl_amd import _native
+    return _native
+
+
+@pytest.fixture(scope="module")
+def lib(nat):
+    return nat.load_library()
+
+
+def _declared():
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(swarm_\w+)\s*\(", text, re.M)))
+
+
+def test_header_symbols_are_exported(nat, lib):
+    declared = _declared()
+    assert declared == sorted(nat.EXPORTED_SYMBOLS)
+    for name in declared:
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", str(nat.LIB_PATH)], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert set(declared) <= exported
+    # nothing else of ours leaks out of the shared object
+    assert {s for s in exported if s.startswith("swarm_")} == set(declared)
+
+
+def test_library_is_built_for_gfx950(nat):
+    data = nat.LIB_PATH.read_bytes()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data  # offload bundle id of the device code
+    assert b"amdgcn-amd-amdhsa--gfx942" not in data  # MI355X only: no other device targets
+
+
+def _params(nat, lib, **kw):
+    p = nat.SwarmParams()
+    lib.swarm_params_default(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def test_abi_version_and_defaults(nat, lib):
+    from swarm_marl_amd.envs.common import DroneEnvConfig
+    assert lib.swarm_abi_version() == nat.ABI_VERSION == 1
+    p = _params(nat, lib)
+    c = DroneEnvConfig()
+    for name in ("max_steps", "num_obstacles", "sensed_obstacles", "neighbor_k"):
+        assert getattr(p, name) == getattr(c, name), name
+    for name in ("world_size", "dt", "max_speed", "max_accel", "collision_radius", "goal_radius",
+                 "obstacle_radius", "desired_spacing", "reward_progress_scale", "reward_goal",
+                 "reward_collision", "reward_formation_scale"):
+        assert getattr(p, name) == getattr(c, name), name
+    assert p.num_drones == 3 and p.dynamics == nat.DYN_KINEMATIC and p.auto_reset == 0
+
+
+@pytest.mark.parametrize("k,ms", [(3, 4), (0, 0), (16, 16), (5, 2)])
+def test_obs_dim(nat, lib, k, ms):
+    p = _params(nat, lib, neighbor_k=k, sensed_obstacles=ms)
+    assert lib.swarm_obs_dim(ctypes.byref(p)) == 9 + 4 * k + 4 * ms
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 16, 33, 63, 64, 65, 100, 256, 1024])
+def test_launch_geometry(nat, lib, n):
+    p = _params(nat, lib, num_drones=n, num_envs=1000)
+    info = nat.SwarmLaunchInfo()
+    assert lib.swarm_query_launch(ctypes.byref(p), ctypes.byref(info)) == 0
+    lanes = 1 << (n - 1).bit_length()
+    assert info.lanes_per_env == lanes
+    if lanes <= 64:  # wave teams: 64/L envs per 64-thread workgroup
+        assert info.threads_per_block == 64 and info.envs_per_block == 64 // lanes
+    else:  # one env per workgroup of L threads
+        assert info.threads_per_block == lanes and info.envs_per_block == 1
+    assert info.blocks == -(-1000 // info.envs_per_block)
+    assert 0 < info.lds_bytes <= 160 * 1024
+    assert info.neighbor_slots == 4 and info.obstacle_slots == 5  # K=3 -> 4 keys, Ms=4 -> 5
+    assert info.obs_dim == 37
+
+
+@pytest.mark.parametrize("field,value,code", [
+    ("abi_version", 2, "EINVAL"), ("num_envs", -1, "EINVAL"), ("num_drones", 0, "ELIMIT"),
+    ("num_drones", 1025, "ELIMIT"), ("neighbor_k", 17, "ELIMIT"), ("sensed_obstacles", 17, "ELIMIT"),
+    ("num_obstacles", -2, "EINVAL"), ("dynamics", 7, "EINVAL"), ("reward_mode", 1, "EINVAL"),
+    ("damping_law", 3, "EINVAL"),
+])
+def test_validation_errors(nat, lib, field, value, code):
+    kw = {field: value}
+    if field == "sensed_obstacles":
+        kw["num_obstacles"] = 20
+    p = _params(nat, lib, **kw)
+    info = nat.SwarmLaunchInfo()
+    rc = lib.swarm_query_launch(ctypes.byref(p), ctypes.byref(info))
+    assert rc == getattr(nat, "SWARM_" + code)
+    assert lib.swarm_last_error()  # a message is set
+    with pytest.raises(ValueError):
+        nat.check(rc, lib)
+
+
+def test_null_arguments_and_empty_batch(nat, lib):
+    p = _params(nat, lib, num_envs=0)
+    s, o = nat.SwarmState(), nat.SwarmOut()
+    assert lib.swarm_step(None, ctypes.byref(s), None, None, ctypes.byref(o), None) == nat.SWARM_ENULL
+    assert lib.swarm_step(ctypes.byref(p), None, None, None, ctypes.byref(o), None) == nat.SWARM_ENULL
+    assert lib.swarm_query_launch(ctypes.byref(p), None) == nat.SWARM_ENULL
+    # zero envs: a valid no-op (returns before any launch)
+    assert lib.swarm_step(ctypes.byref(p), ctypes.byref(s), None, None, ctypes.byref(o), None) == 0
+    assert lib.swarm_reset(ctypes.byref(p), ctypes.byref(s), None, ctypes.byref(o), None) == 0
+    assert lib.swarm_observe(ctypes.byref(p), ctypes.byref(s), None, ctypes.byref(o), None) == 0
+    # non-empty batch with missing buffers: rejected before any launch
+    p2 = _params(nat, lib, num_envs=4)
+    assert lib.swarm_step(ctypes.byref(p2), ctypes.byref(s), None, None, ctypes.byref(o), None) == nat.SWARM_ENULL
+    assert b"NULL" in lib.swarm_last_error()
+
+
+def test_missing_library_fails_loudly(nat, tmp_path):
+    with pytest.raises(nat.NativeLibraryError):
+        nat.load_library(tmp_path / "libswarm_mi355x.so")
