@@ -92,7 +92,7 @@ constexpr float FAST_HI = 1.0f + 0x1p-18f;
 // Derived, launch-ready parameters (host computes once per call).
 struct KParams {
   int E, N, M, K, Ms, D, max_steps, auto_reset, substeps, damping_law;
-  int log2_lanes, envs_per_block, chunk_rows, obs_vec4;
+  int log2_lanes, envs_per_block, chunk_rows, obs_vec4, pack_bytes;
   int off_obst, off_stage, obst_stride, ring;   // ring: pos4 slots per team (2L wave, L block)
   uint32_t nb_keep, ob_keep;        // key masks: high bits kept from the distance, low bits = index
   long long env_offset;
@@ -384,12 +384,14 @@ __device__ __forceinline__ bool finish_keys(const uint32_t (&k)[S], const float4
   return dlb > wd[K - 1];
 }
 
-// arr[idx] of a register array without dynamic indexing (which would move it to scratch)
+// Largest of the first K entries of a register array (= entry K-1 of a sorted list), as a
+// reduction: a select chain on the index gets folded back into a dynamic alloca index, which
+// moves the whole array to scratch.
 template <int S>
-__device__ __forceinline__ float reg_at(const float (&arr)[S], int idx) {
-  float v = arr[0];
+__device__ __forceinline__ float max_first(const float (&arr)[S], int K) {
+  float v = 0.f;
 #pragma unroll
-  for (int u = 1; u < S; ++u) v = (u == idx) ? arr[u] : v;
+  for (int u = 0; u < S; ++u) v = (u < K) ? fmaxf(v, arr[u]) : v;
   return v;
 }
 
@@ -468,6 +470,10 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   float4* obst4 = reinterpret_cast<float4*>(smem + P.off_obst) + team * P.obst_stride;
   float* stage = reinterpret_cast<float*>(smem + P.off_stage);
   uint64_t team_bits = 0;
+  // one env of exactly 64 agents per wave: the per-agent byte outputs (terminated, truncated,
+  // active) leave as three 64-B dword stores built from wave ballots instead of 3 x 64 byte stores
+  const bool packed_bytes = W64 && KIND == KIND_STEP && P.pack_bytes;
+  bool new_act_out = false;
   if constexpr (WAVE) team_bits = (W64 || L == 64) ? ~0ull : (((1ull << L) - 1ull) << (team * L));
 
   // envs this call writes: every env (step) or the masked ones (reset / observe)
@@ -682,10 +688,10 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       if constexpr (MSL > 0) slow_ob = !finish_keys<MSL, true, false>(ok, obst4, M, 0, 0x7fffffff, Mse, P.ob_keep, false, px, py, pz, od, oj);
     }
     if constexpr (KS > 0) {
-      if (slow_nb) exact_select<NW, false>(ring, N, t, Kq, reg_at(wd, Kq - 1), px, py, pz, wd, wj);
+      if (slow_nb) exact_select<NW, false>(ring, N, t, Kq, max_first(wd, Kq), px, py, pz, wd, wj);
     }
     if constexpr (MSL > 0) {
-      if (slow_ob) exact_select<OW, true>(obst4, M, -1, Mse, reg_at(od, Mse - 1), px, py, pz, od, oj);
+      if (slow_ob) exact_select<OW, true>(obst4, M, -1, Mse, max_first(od, Mse), px, py, pz, od, oj);
     }
   };
   // the step's kinematic pass ranks by d~, every other pass by s'
@@ -787,8 +793,10 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     // per-agent step outputs (the episode that just ended, for reset envs)
     if (is_agent) {
       O.reward[ag] = rew;
-      O.terminated[ag] = term ? 1 : 0;
-      O.truncated[ag] = trunc ? 1 : 0;
+      if (!packed_bytes) {
+        O.terminated[ag] = term ? 1 : 0;
+        O.truncated[ag] = trunc ? 1 : 0;
+      }
       if (O.dist_goal) O.dist_goal[ag] = dist_out;
       if (O.info_flags)
         O.info_flags[ag] = (uint8_t)((act ? SWARM_AGENT_STEPPED : 0u) | (act && reached ? SWARM_AGENT_REACHED : 0u) |
@@ -841,7 +849,8 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       if (do_reset) new_act = true;
       S.pos[ag * 3 + 0] = px; S.pos[ag * 3 + 1] = py; S.pos[ag * 3 + 2] = pz;
       S.vel[ag * 3 + 0] = vx; S.vel[ag * 3 + 1] = vy; S.vel[ag * 3 + 2] = vz;
-      S.active[ag] = new_act ? 1 : 0;
+      if (!packed_bytes) S.active[ag] = new_act ? 1 : 0;
+      new_act_out = new_act;
       if (DYN == DYN_PHYS && do_reset) S.damping[ag] = damp;
     } else if (sel) {
       if (O.dist_goal) O.dist_goal[ag] = dist_out;
@@ -857,6 +866,17 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       gs[3 * t + 0] = px; gs[3 * t + 1] = py; gs[3 * t + 2] = pz;
       gs[3 * N + 3 * t + 0] = vx; gs[3 * N + 3 * t + 1] = vy; gs[3 * N + 3 * t + 2] = vz;
       if (t == 0) { gs[6 * N + 0] = gx; gs[6 * N + 1] = gy; gs[6 * N + 2] = gz; }
+    }
+  }
+  if (packed_bytes && env_ok) {  // wave-uniform (W64: the block is one env)
+    const uint64_t mt = __ballot(term), mr = __ballot(trunc), ma = __ballot(new_act_out);
+    const int grp = t >> 4;
+    if (grp < 3) {
+      const uint64_t m = grp == 0 ? mt : (grp == 1 ? mr : ma);
+      const uint32_t nib = (uint32_t)(m >> (4 * (t & 15))) & 0xFu;
+      const uint32_t word = (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
+      uint8_t* base = grp == 0 ? O.terminated : (grp == 1 ? O.truncated : S.active);
+      *reinterpret_cast<uint32_t*>(base + env * 64 + 4 * (t & 15)) = word;
     }
   }
   const bool new_episode = (mode == MODE_STEP) ? do_reset : (mode == MODE_RESET && sel);
@@ -1202,6 +1222,9 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
       return fail(SWARM_ENULL, "out.reward/terminated/truncated/env_done required by swarm_step");
   }
   if (((uintptr_t)o->obs) % 16 != 0) kp.obs_vec4 = 0;
+  // ballot-packed byte outputs need N == 64 and dword-aligned bool tensors
+  kp.pack_bytes = (kp.N == 64 && mode == MODE_STEP && ((uintptr_t)o->terminated | (uintptr_t)o->truncated |
+                                                       (uintptr_t)s->active) % 4 == 0) ? 1 : 0;
   const int lanes = 1 << kp.log2_lanes;
   const int lm = lanes > 64 ? 0 : (lanes == 64 ? 2 : 1);
   const int ks = info.neighbor_slots, msl = info.obstacle_slots;

@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=${1:-r01}
 OUT=gpurun_out/$R
-mkdir -p "$OUT"
+mkdir -p "$OUT/pmc"
 export TMPDIR=/tmp
 BENCH_ARGS=${BENCH_ARGS:-"--no-cpu-baseline"}
 echo "== bench (plain)"
