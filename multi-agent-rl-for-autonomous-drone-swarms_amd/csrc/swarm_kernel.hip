@@ -1020,11 +1020,17 @@ kernel_fn pick_ks(int ks, int msl) {
 }
 template <int KIND, int DYN>
 void* pick_lm(int lm, int ks, int msl) {
+#ifdef SWARM_DEV_HOT
+  // diagnostic builds (tools/): only the headline instantiation (N = 64, K = 3, Ms = 4)
+  if (lm == 2 && ks == 4 && msl == 5) return reinterpret_cast<void*>(swarm_kernel<KIND, DYN, 4, 5, 2>);
+  return nullptr;
+#else
   switch (lm) {
     case 0: return reinterpret_cast<void*>(pick_ks<KIND, DYN, 0>(ks, msl));
     case 1: return reinterpret_cast<void*>(pick_ks<KIND, DYN, 1>(ks, msl));
     default: return reinterpret_cast<void*>(pick_ks<KIND, DYN, 2>(ks, msl));
   }
+#endif
 }
 
 }  // namespace
@@ -1232,6 +1238,7 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   void* fnp = (mode == MODE_STEP) ? (kin ? swarm_pick_0(lm, ks, msl) : swarm_pick_1(lm, ks, msl))
                                   : (kin ? swarm_pick_2(lm, ks, msl) : swarm_pick_3(lm, ks, msl));
   kernel_fn fn = reinterpret_cast<kernel_fn>(fnp);
+  if (!fn) return fail(SWARM_ELIMIT, "no kernel instantiation for lanes=%d ks=%d msl=%d in this build", lanes, ks, msl);
   if (info.lds_bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        info.lds_bytes);
