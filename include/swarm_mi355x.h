@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SWARM_ABI_VERSION 1
+#define SWARM_ABI_VERSION 2
 
 /* error codes */
 #define SWARM_OK 0
@@ -51,6 +51,14 @@ extern "C" {
 /* reward modes */
 #define SWARM_REW_SWARM 0    /* progress + formation + goal + collision (drone_swarm_env.py:137-172) */
 #define SWARM_REW_PHYSICS 1  /* -0.1*dist, -10 collision, +50 goal (drone_physics_env.py:374-417) */
+
+/* kernel selection (swarm_params_t.kernel_path) */
+#define SWARM_PATH_AUTO 0     /* specialised kernels where they apply (swarm_step64 for the headline shape) */
+#define SWARM_PATH_GENERIC 1  /* always the generic swarm_kernel (A/B parity checks, diagnostics) */
+
+/* kernel actually launched (swarm_launch_info_t.kernel_id) */
+#define SWARM_KERNEL_GENERIC 0  /* swarm_kernel<KIND, DYN, KS, MSL, LM> */
+#define SWARM_KERNEL_STEP64 1   /* swarm_step64: N = 64, K = 3, Ms = 4, 4 <= M <= 16, kinematic step */
 
 /* env_done bits ([E] u8) */
 #define SWARM_ENV_TERMINATED 1u  /* terminated["__all__"] */
@@ -101,6 +109,8 @@ typedef struct swarm_params {
   double substep_dt;         /* 1/240 */
   double drone_contact_radius;    /* contact approximation radius of the 0.3x0.3x0.05 box */
   double ground_contact_height;   /* z at or below which the box touches the plane */
+  int32_t kernel_path;       /* SWARM_PATH_* (default AUTO) */
+  int32_t reserved0;         /* must be 0 */
 } swarm_params_t;
 
 /* Per-env state, device SoA blocks (all dense, C-contiguous). */
@@ -138,6 +148,7 @@ typedef struct swarm_launch_info {
   int32_t obstacle_slots;
   int32_t obs_dim;
   int32_t staged_obs;       /* 1: obs staged through LDS and stored coalesced */
+  int32_t kernel_id;        /* SWARM_KERNEL_* swarm_step launches for these params (aligned buffers) */
 } swarm_launch_info_t;
 
 int swarm_abi_version(void);

@@ -37,7 +37,8 @@
 
 // Build partitioning: the kernel instantiations are compiled as parallel translation units.
 // SWARM_PART k in 0..3 holds the kernels of (KIND, DYN) = (k >> 1, k & 1); SWARM_PART 4 holds
-// the host side and the C-ABI; SWARM_PART -1 (default) is everything in one unit (tools/).
+// the host side and the C-ABI; SWARM_PART 5 the headline specialisation swarm_step64;
+// SWARM_PART -1 (default) is everything in one unit (tools/).
 #ifndef SWARM_PART
 #define SWARM_PART -1
 #endif
@@ -996,7 +997,297 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
 #endif
 }
 
+// ------------------------------------------------------------------ step64: the headline kernel
+// Specialisation of the step for one env of exactly 64 drones per 64-lane wave, kinematic
+// dynamics + swarm reward, K = 3 neighbours, Ms = 4 sensed obstacles, 4 <= M <= 16 obstacles
+// (DroneEnvConfig defaults at N = 64: SURVEY.md §8d config 3).  Same phases, numerics and helper
+// functions as swarm_kernel<0, 0, 4, 5, 2>; outputs are bit-identical to it
+// (tests/test_gpu_step64.py).  Laid out for 8 waves per SIMD (<= 64 VGPRs, < 5 KB LDS per wave)
+// so that every wave of the 8192-env headline launch is resident at once:
+//  * env-uniform data (goal, step counter, episode, base addresses) lives in SGPRs and per-lane
+//    addresses are 32-bit offsets from them (no per-lane 64-bit address arithmetic);
+//  * a 96-entry position ring (drone j at j, and at j + 64 for j < 32): rotation r reads
+//    ring[t + r] as base + immediate;
+//  * the observation row is built in registers once, staged in LDS CH rows at a time and stored
+//    with coalesced 16-B global stores.
+constexpr int S64_N = 64;
+constexpr int S64_K = 3;
+constexpr int S64_MS = 4;
+constexpr int S64_D = 9 + 4 * S64_K + 4 * S64_MS;  // 37
+constexpr int S64_MMAX = 16;
+constexpr int S64_RING = 96;
+constexpr int S64_CH = 16;  // obs rows per LDS staging chunk (multiple of 4: 16-B aligned chunks)
+
+template <int CH>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
+swarm_step64(const KParams P, const swarm_state_t S, const float* __restrict__ actions,
+             const uint8_t* __restrict__ amask, const swarm_out_t O) {
+  constexpr int KS = S64_K + 1, MSL = S64_MS + 1, D = S64_D;
+  static_assert(CH % 4 == 0 && S64_N % CH == 0, "chunk rows");
+  __shared__ float4 ring[S64_RING];
+  __shared__ float4 obst[S64_MMAX];
+  __shared__ __attribute__((aligned(16))) float stage[CH * D];
+  const int t = threadIdx.x;
+  const int env = blockIdx.x;
+  const int M = P.M;
+  const unsigned t3 = 3u * (unsigned)t;
+  const size_t ea = (size_t)env * S64_N;  // first agent of the env (uniform)
+  float* __restrict__ posE = S.pos + ea * 3;
+  float* __restrict__ velE = S.vel + ea * 3;
+  const float* __restrict__ actE = actions + ea * 3;
+  STAMP(0);
+#ifdef SWARM_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) g_stamps[blockIdx.x * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+#endif
+
+  // ---- load: env-uniform scalars, per-lane rows, obstacles to LDS
+  float gx = S.goal[3 * env + 0], gy = S.goal[3 * env + 1], gz = S.goal[3 * env + 2];
+  const int stepc = S.step_count[env];
+  const uint32_t episode0 = S.episode[env];
+  float ax = actE[t3], ay = actE[t3 + 1], az = actE[t3 + 2];
+  const bool has = (amask == nullptr) || ((amask + ea)[t] != 0);
+  float px = posE[t3], py = posE[t3 + 1], pz = posE[t3 + 2];
+  float vx = velE[t3], vy = velE[t3 + 1], vz = velE[t3 + 2];
+  bool act = (S.active + ea)[t] != 0;
+  if (t < M) {
+    const float* o = S.obstacles + ((size_t)env * M) * 3 + t3;
+    obst[t] = make_float4(o[0], o[1], o[2], 0.f);
+  }
+  const int n_active = __popcll(__ballot(act));
+  STAMP(1);
+
+  // ---- integrate: drone_swarm_env.py:98-117 (identical to swarm_kernel, DYN_KIN)
+  float prev_d = 0.f;
+  if (act) {
+    prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
+    if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
+    ax = fminf(fmaxf(ax, -1.f), 1.f) * P.amax;
+    ay = fminf(fmaxf(ay, -1.f), 1.f) * P.amax;
+    az = fminf(fmaxf(az, -1.f), 1.f) * P.amax;
+    vx = vx + ax * P.dt;
+    vy = vy + ay * P.dt;
+    vz = vz + az * P.dt;
+    const float sp = sqrt_rn(sqsum_1d(vx, vy, vz));
+    if (!(sp <= P.vmax || sp < (float)1e-8)) {
+      vx = (vx / sp) * P.vmax;
+      vy = (vy / sp) * P.vmax;
+      vz = (vz / sp) * P.vmax;
+    }
+    px = px + vx * P.dt;
+    py = py + vy * P.dt;
+    pz = pz + vz * P.dt;
+  }
+  if (n_active > 0) {
+    px = fminf(fmaxf(px, P.neg_half_w), P.half_w);
+    py = fminf(fmaxf(py, P.neg_half_w), P.half_w);
+    pz = fminf(fmaxf(pz, P.neg_half_w), P.half_w);
+  }
+  {
+    const float4 me = make_float4(px, py, pz, act ? 1.f : 0.f);
+    ring[t] = me;
+    if (t < S64_RING - S64_N) ring[t + S64_N] = me;
+  }
+  __syncthreads();
+  STAMP(2);
+
+  // ---- pair + obstacle passes
+  uint32_t nk[KS], ok[MSL];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
+#pragma unroll
+  for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
+  bool ocoll = false;
+  float smin = __builtin_inff();
+  double fsum = 0.0;
+  const bool fast = __all(act);
+  if (fast) pair_pass_w64<KS, 1, true>(ring, t, px, py, pz, true, P.nb_keep, P.ds_f, nk, smin, fsum);
+  else pair_pass_w64<KS, 1, false>(ring, t, px, py, pz, act, P.nb_keep, P.ds_f, nk, smin, fsum);
+  obstacle_pass<MSL, true>(obst, M, px, py, pz, act, P.s_obst, P.ob_keep, ok, ocoll);
+  STAMP(3);
+
+  // ---- exact top-K (finish_keys, rare exact_select)
+  float wd[KS], od[MSL];
+  int wj[KS], oj[MSL];
+  auto select_topk = [&](bool dkey) {
+    const bool slow_nb = !finish_keys<KS, false, true>(nk, ring, S64_N, t, S64_N - 1, S64_K, P.nb_keep, dkey, px, py,
+                                                       pz, wd, wj);
+    const bool slow_ob = !finish_keys<MSL, true, false>(ok, obst, M, 0, 0x7fffffff, S64_MS, P.ob_keep, false, px, py,
+                                                        pz, od, oj);
+    if (slow_nb) exact_select<KS, false>(ring, S64_N, t, S64_K, max_first(wd, S64_K), px, py, pz, wd, wj);
+    if (slow_ob) exact_select<MSL, true>(obst, M, -1, S64_MS, max_first(od, S64_MS), px, py, pz, od, oj);
+  };
+  select_topk(true);
+  STAMP(4);
+
+  // ---- rewards / terminations: drone_swarm_env.py:120-172
+  bool pcoll;
+  if (fast) {
+    pcoll = wd[0] <= P.thr_pair;
+  } else {
+    pcoll = smin <= P.thr_pair * FAST_LO;
+    if (!pcoll && smin <= P.thr_pair * FAST_HI && act)
+      pcoll = exact_pair_collision(ring, S64_N, t, px, py, pz, P.s_pair);
+  }
+  const float curr = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
+  float rew = 0.f;
+  bool reached = false, collided = false;
+  if (act) {
+    reached = (double)curr <= P.goal_radius;
+    collided = ocoll || pcoll;
+    double r = ((double)prev_d - (double)curr) * P.kp;
+    if (n_active > 1) r = r + (-P.kf) * (fsum / (double)(n_active - 1));
+    if (reached) r = r + P.r_goal;
+    if (collided) r = r + P.r_col;
+    rew = (float)r;
+  }
+  const bool any_c = __ballot(act && collided) != 0;
+  const bool any_cand = __ballot(act && !reached && !collided) != 0;
+  bool term = false, trunc = false, cont = false, term_all = false, trunc_all = false;
+  int new_step = stepc;
+  if (n_active == 0) {  // drone_swarm_env.py:93-95
+    term_all = true;
+  } else {
+    new_step = stepc + 1;
+    const bool tl = new_step >= P.max_steps;
+    term_all = (!any_cand && !any_c && !tl) || any_c;
+    trunc_all = tl && !term_all;
+    if (act) {
+      const bool done_i = reached || collided;
+      term = done_i;
+      trunc = tl && !done_i;
+      cont = !done_i && !tl && !any_c;
+    }
+  }
+  const bool do_reset = P.auto_reset && (term_all || trunc_all) && !(SWARM_ABLATE & ABL_RESET);
+  (O.reward + ea)[t] = rew;
+  if (O.dist_goal) (O.dist_goal + ea)[t] = curr;
+  if (O.info_flags)
+    (O.info_flags + ea)[t] = (uint8_t)((act ? SWARM_AGENT_STEPPED : 0u) | (act && reached ? SWARM_AGENT_REACHED : 0u) |
+                                       (act && collided ? SWARM_AGENT_COLLISION : 0u) |
+                                       (cont ? SWARM_AGENT_HAS_OBS : 0u));
+  if (t == 0)
+    O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
+                                (do_reset ? SWARM_ENV_RESET : 0u));
+  const uint64_t m_term = __ballot(term), m_trunc = __ballot(trunc);
+  STAMP(5);
+
+  // ---- in-kernel auto-reset (wave-uniform): new episode, then its key passes
+  uint32_t episode_new = episode0;
+  if (do_reset) {
+    const long long genv = P.env_offset + env;
+    episode_new = episode0 + 1u;
+    uint32_t w[4];
+    draw_block(P, genv, episode_new, (uint32_t)t, w);
+    px = uni(w[0], P.neg_half_w, P.width_w);
+    py = uni(w[1], P.neg_half_w, P.width_w);
+    pz = uni(w[2], P.neg_half_w, P.width_w);
+    vx = vy = vz = 0.f;
+    act = true;
+    __syncthreads();  // every read of the old ring / obstacles is done
+    if (t < M) {
+      draw_block(P, genv, episode_new, (uint32_t)(S64_N + t), w);
+      obst[t] = make_float4(uni(w[0], P.neg_half_w, P.width_w), uni(w[1], P.neg_half_w, P.width_w),
+                            uni(w[2], P.neg_half_w, P.width_w), 0.f);
+    }
+    draw_block(P, genv, episode_new, (uint32_t)(S64_N + M), w);
+    gx = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(uni(w[0], P.neg_half_w, P.width_w))));
+    gy = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(uni(w[1], P.neg_half_w, P.width_w))));
+    gz = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(uni(w[2], P.neg_half_w, P.width_w))));
+    const float4 me = make_float4(px, py, pz, 1.f);
+    ring[t] = me;
+    if (t < S64_RING - S64_N) ring[t + S64_N] = me;
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
+#pragma unroll
+    for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
+    bool c2 = false;
+    float s2 = 0.f;
+    double f2 = 0.0;
+    pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
+    obstacle_pass<MSL, false>(obst, M, px, py, pz, false, 0.f, P.ob_keep, ok, c2);
+    select_topk(false);
+  }
+
+  STAMP(6);
+  // ---- state write-back
+  const bool new_act = do_reset || cont;
+  posE[t3] = px; posE[t3 + 1] = py; posE[t3 + 2] = pz;
+  velE[t3] = vx; velE[t3 + 1] = vy; velE[t3 + 2] = vz;
+  {  // terminated, truncated, active: three 64-B rows of bytes built from wave ballots
+    const uint64_t m_act = __ballot(new_act);
+    const int grp = t >> 4;
+    if (grp < 3) {
+      const uint64_t m = grp == 0 ? m_term : (grp == 1 ? m_trunc : m_act);
+      const uint32_t nib = (uint32_t)(m >> (4 * (t & 15))) & 0xFu;
+      const uint32_t word = (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
+      uint8_t* base = grp == 0 ? O.terminated : (grp == 1 ? O.truncated : S.active);
+      *reinterpret_cast<uint32_t*>(base + ea + 4 * (t & 15)) = word;
+    }
+  }
+  if (t == 0) {
+    S.step_count[env] = do_reset ? 0 : new_step;
+    if (do_reset) {
+      S.episode[env] = episode_new;
+      S.goal[3 * env + 0] = gx; S.goal[3 * env + 1] = gy; S.goal[3 * env + 2] = gz;
+    }
+  }
+  if (do_reset && t < M) {
+    float* o = S.obstacles + ((size_t)env * M) * 3 + t3;
+    const float4 q = obst[t];
+    o[0] = q.x; o[1] = q.y; o[2] = q.z;
+  }
+  if (O.global_state) {
+    float* gs = O.global_state + (size_t)env * (6 * S64_N + 3);
+    gs[t3] = px; gs[t3 + 1] = py; gs[t3 + 2] = pz;
+    gs[3 * S64_N + t3] = vx; gs[3 * S64_N + t3 + 1] = vy; gs[3 * S64_N + t3 + 2] = vz;
+    if (t == 0) { gs[6 * S64_N + 0] = gx; gs[6 * S64_N + 1] = gy; gs[6 * S64_N + 2] = gz; }
+  }
+
+  STAMP(7);
+  // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)] (drone_swarm_env.py:226-291)
+  float row[D];
+  row[0] = px; row[1] = py; row[2] = pz;
+  row[3] = vx; row[4] = vy; row[5] = vz;
+  row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
+#pragma unroll
+  for (int s = 0; s < S64_K; ++s) {
+    const float4 q = ring[wj[s] & (S64_N - 1)];
+    row[9 + 4 * s] = q.x - px; row[10 + 4 * s] = q.y - py; row[11 + 4 * s] = q.z - pz; row[12 + 4 * s] = wd[s];
+  }
+#pragma unroll
+  for (int s = 0; s < S64_MS; ++s) {
+    const float4 q = obst[oj[s] & (S64_MMAX - 1)];
+    row[21 + 4 * s] = q.x - px; row[22 + 4 * s] = q.y - py; row[23 + 4 * s] = q.z - pz; row[24 + 4 * s] = od[s];
+  }
+  if (SWARM_ABLATE & ABL_OBS) return;
+  constexpr int V4 = CH * D / 4;  // float4 per chunk
+  float4* __restrict__ dst = reinterpret_cast<float4*>(O.obs + ea * D);
+  const float4* s4 = reinterpret_cast<const float4*>(stage);
+  float* srow = stage + (t % CH) * D;
+#pragma unroll
+  for (int c = 0; c < S64_N / CH; ++c) {
+    if (t / CH == c) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) srow[i] = row[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = t; i < V4; i += 64) dst[c * V4 + i] = s4[i];
+    __syncthreads();
+  }
+  STAMP(8);
+#ifdef SWARM_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) {
+    g_stamps[blockIdx.x * 16 + 9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+    g_stamps[blockIdx.x * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    g_stamps[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
+}
+
 // ------------------------------------------------------------------ host side
+typedef void (*step64_fn)(const KParams, const swarm_state_t, const float*, const uint8_t*, const swarm_out_t);
 typedef void (*kernel_fn)(const KParams, const swarm_state_t, const float*, const uint8_t*, const swarm_out_t,
                           const uint8_t*, int);
 
@@ -1041,6 +1332,11 @@ SWARM_PICK_DECL(0);
 SWARM_PICK_DECL(1);
 SWARM_PICK_DECL(2);
 SWARM_PICK_DECL(3);
+// the headline specialisation (SWARM_PART 5)
+__attribute__((visibility("hidden"))) void* swarm_pick_step64();
+#if SWARM_HAS_PART(5)
+__attribute__((visibility("hidden"))) void* swarm_pick_step64() { return reinterpret_cast<void*>(swarm_step64<S64_CH>); }
+#endif
 #if SWARM_HAS_PART(0)
 SWARM_PICK_DECL(0) { return pick_lm<KIND_STEP, DYN_KIN>(lm, ks, msl); }
 #endif
@@ -1110,6 +1406,13 @@ int obs_dim_of(const swarm_params_t* p) {
   return 9 + 4 * (p->neighbor_k > 0 ? p->neighbor_k : 0) + 4 * (p->sensed_obstacles > 0 ? p->sensed_obstacles : 0);
 }
 
+// The headline specialisation swarm_step64 covers N = 64, K = 3, Ms = 4, 4 <= M <= 16 in
+// kinematic/swarm mode (buffer alignment is checked at launch).
+bool step64_applies(const swarm_params_t* p, const KParams& k) {
+  return p->kernel_path == SWARM_PATH_AUTO && k.N == S64_N && k.K == S64_K && k.Ms == S64_MS && k.M >= S64_MS &&
+         k.M <= S64_MMAX && p->dynamics == DYN_KIN;
+}
+
 int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* info) {
   if (!p) return fail(SWARM_ENULL, "params is NULL");
   if (p->abi_version != SWARM_ABI_VERSION)
@@ -1128,6 +1431,8 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
     return fail(SWARM_EINVAL, "dynamics/reward_mode pairing must be kinematic+swarm or physics+physics");
   if (p->dynamics == DYN_PHYS && p->physics_substeps < 0) return fail(SWARM_EINVAL, "physics_substeps < 0");
   if (p->damping_law != 0 && p->damping_law != 1) return fail(SWARM_EINVAL, "damping_law must be 0 or 1");
+  if (p->kernel_path != SWARM_PATH_AUTO && p->kernel_path != SWARM_PATH_GENERIC)
+    return fail(SWARM_EINVAL, "kernel_path must be SWARM_PATH_AUTO or SWARM_PATH_GENERIC (got %d)", p->kernel_path);
 
   KParams k;
   memset(&k, 0, sizeof(k));
@@ -1205,6 +1510,7 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
     info->obstacle_slots = obstacle_slots(k.Ms, k.M);
     info->obs_dim = k.D;
     info->staged_obs = 1;
+    info->kernel_id = SWARM_KERNEL_GENERIC;
   }
   return SWARM_OK;
 }
@@ -1231,6 +1537,13 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   // ballot-packed byte outputs need N == 64 and dword-aligned bool tensors
   kp.pack_bytes = (kp.N == 64 && mode == MODE_STEP && ((uintptr_t)o->terminated | (uintptr_t)o->truncated |
                                                        (uintptr_t)s->active) % 4 == 0) ? 1 : 0;
+  if (mode == MODE_STEP && step64_applies(p, kp) && kp.obs_vec4 && kp.pack_bytes) {
+    hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step64()), dim3(kp.E), dim3(64), 0, (hipStream_t)stream,
+                       kp, *s, actions, amask, *o);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
+    return SWARM_OK;
+  }
   const int lanes = 1 << kp.log2_lanes;
   const int lm = lanes > 64 ? 0 : (lanes == 64 ? 2 : 1);
   const int ks = info.neighbor_slots, msl = info.obstacle_slots;
@@ -1299,6 +1612,7 @@ void swarm_params_default(swarm_params_t* p) {
   p->substep_dt = 1.0 / 240.0;
   p->drone_contact_radius = 0.15;
   p->ground_contact_height = 0.025;
+  p->kernel_path = SWARM_PATH_AUTO;
 }
 
 int swarm_obs_dim(const swarm_params_t* p) {
@@ -1309,7 +1623,16 @@ int swarm_obs_dim(const swarm_params_t* p) {
 int swarm_query_launch(const swarm_params_t* p, swarm_launch_info_t* info) {
   KParams kp;
   if (!info) return fail(SWARM_ENULL, "info is NULL");
-  return build_kparams(p, &kp, info);
+  const int rc = build_kparams(p, &kp, info);
+  if (rc == SWARM_OK && step64_applies(p, kp)) {  // geometry of the step launch (reset/observe stay generic)
+    info->threads_per_block = 64;
+    info->envs_per_block = 1;
+    info->lanes_per_env = 64;
+    info->blocks = kp.E;
+    info->lds_bytes = (int)(sizeof(float4) * (S64_RING + S64_MMAX) + sizeof(float) * S64_CH * S64_D);
+    info->kernel_id = SWARM_KERNEL_STEP64;
+  }
+  return rc;
 }
 
 int swarm_step(const swarm_params_t* p, const swarm_state_t* s, const float* actions, const uint8_t* action_mask,

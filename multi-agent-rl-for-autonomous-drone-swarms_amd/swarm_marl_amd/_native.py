@@ -14,7 +14,12 @@ LIB_NAME = "libswarm_mi355x.so"
 LIB_DIR = Path(__file__).resolve().parent / "_lib"
 LIB_PATH = LIB_DIR / LIB_NAME
 
-ABI_VERSION = 1
+ABI_VERSION = 2
+
+PATH_AUTO = 0
+PATH_GENERIC = 1
+KERNEL_GENERIC = 0
+KERNEL_STEP64 = 1
 
 SWARM_OK = 0
 SWARM_EINVAL = -1
@@ -80,6 +85,8 @@ class SwarmParams(ctypes.Structure):
         ("substep_dt", ctypes.c_double),
         ("drone_contact_radius", ctypes.c_double),
         ("ground_contact_height", ctypes.c_double),
+        ("kernel_path", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
     ]
 
 
@@ -97,7 +104,7 @@ class SwarmOut(ctypes.Structure):
 class SwarmLaunchInfo(ctypes.Structure):
     _fields_ = [(name, ctypes.c_int32) for name in
                 ("threads_per_block", "envs_per_block", "lanes_per_env", "blocks", "lds_bytes",
-                 "neighbor_slots", "obstacle_slots", "obs_dim", "staged_obs")]
+                 "neighbor_slots", "obstacle_slots", "obs_dim", "staged_obs", "kernel_id")]
 
 
 _LIB = None

@@ -37,7 +37,8 @@ class VecSwarm:
                  num_drones: int | None = None, dynamics: str = "kinematic",
                  auto_reset: bool = True, seed: int = 0, env_offset: int = 0,
                  device: str | torch.device | None = None, with_infos: bool = False,
-                 with_global_state: bool = False, physics: dict[str, Any] | None = None):
+                 with_global_state: bool = False, physics: dict[str, Any] | None = None,
+                 kernel_path: str = "auto"):
         if isinstance(config, DroneEnvConfig):
             cfg, raw = config, {}
         else:
@@ -76,6 +77,9 @@ class VecSwarm:
         p.damping_law = int(phys["damping_law"])
         p.env_offset = int(env_offset)
         p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        if kernel_path not in ("auto", "generic"):
+            raise ValueError(f"kernel_path must be 'auto' or 'generic', got {kernel_path!r}")
+        p.kernel_path = nat.PATH_AUTO if kernel_path == "auto" else nat.PATH_GENERIC
         for name in ("world_size", "dt", "max_speed", "max_accel", "collision_radius",
                      "goal_radius", "obstacle_radius", "desired_spacing", "reward_progress_scale",
                      "reward_goal", "reward_collision", "reward_formation_scale"):
@@ -215,9 +219,12 @@ class VecSwarm:
         return d
 
     def kernel_name(self) -> str:
-        """Template instantiation the step launches: swarm_kernel<KIND, DYN, KS, MSL, LM>
-        (KIND 0 = step; LM lane mode 0 block / 1 multi-team wave / 2 one team per wave)."""
+        """Kernel the step launches: swarm_step64<16> (headline specialisation) or the generic
+        swarm_kernel<KIND, DYN, KS, MSL, LM> (KIND 0 = step; LM lane mode 0 block / 1
+        multi-team wave / 2 one team per wave)."""
         li = self.launch_info
+        if int(li.kernel_id) == nat.KERNEL_STEP64:
+            return "swarm_step64<16>"
         lanes = int(li.lanes_per_env)
         lm = 0 if lanes > 64 else (2 if lanes == 64 else 1)
         return (f"swarm_kernel<0, {int(self.params.dynamics)}, {int(li.neighbor_slots)}, "

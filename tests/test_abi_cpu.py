@@ -60,7 +60,7 @@ def _params(nat, lib, **kw):
 
 def test_abi_version_and_defaults(nat, lib):
     from swarm_marl_amd.envs.common import DroneEnvConfig
-    assert lib.swarm_abi_version() == nat.ABI_VERSION == 1
+    assert lib.swarm_abi_version() == nat.ABI_VERSION == 2
     p = _params(nat, lib)
     c = DroneEnvConfig()
     for name in ("max_steps", "num_obstacles", "sensed_obstacles", "neighbor_k"):
@@ -96,10 +96,10 @@ def test_launch_geometry(nat, lib, n):
 
 
 @pytest.mark.parametrize("field,value,code", [
-    ("abi_version", 2, "EINVAL"), ("num_envs", -1, "EINVAL"), ("num_drones", 0, "ELIMIT"),
+    ("abi_version", 1, "EINVAL"), ("num_envs", -1, "EINVAL"), ("num_drones", 0, "ELIMIT"),
     ("num_drones", 1025, "ELIMIT"), ("neighbor_k", 17, "ELIMIT"), ("sensed_obstacles", 17, "ELIMIT"),
     ("num_obstacles", -2, "EINVAL"), ("dynamics", 7, "EINVAL"), ("reward_mode", 1, "EINVAL"),
-    ("damping_law", 3, "EINVAL"),
+    ("damping_law", 3, "EINVAL"), ("kernel_path", 2, "EINVAL"),
 ])
 def test_validation_errors(nat, lib, field, value, code):
     kw = {field: value}
