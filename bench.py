@@ -45,6 +45,10 @@ def parse():
     ap.add_argument("--ring", type=int, default=8, help="distinct pre-generated action tensors")
     ap.add_argument("--cpu-seconds", type=float, default=3.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--waves-per-simd", type=int, default=0,
+                    help="persistent step kernel: resident waves per SIMD (0 = library default)")
+    ap.add_argument("--no-persistent", action="store_true",
+                    help="one workgroup per env instead of the persistent env queue")
     ap.add_argument("--ctde", action="store_true",
                     help="also emit global_state and all-gather it every step (config 5)")
     return ap.parse_args()
@@ -113,7 +117,8 @@ def main():
     if args.no_term:
         raw.update(collision_radius=0.0, obstacle_radius=0.0, goal_radius=0.0)
     vec = VecSwarm(e, raw, device=dev, auto_reset=True, seed=0, env_offset=rank * e,
-                   with_global_state=args.ctde)
+                   with_global_state=args.ctde, persistent=not args.no_persistent,
+                   waves_per_simd=args.waves_per_simd)
     vec.reset()
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     ring = [torch.rand((e, n, 3), device=dev, generator=gen) * 2 - 1 for _ in range(args.ring)]
@@ -175,6 +180,7 @@ def main():
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "kernel_ms_mean": kern_ms, "kernel_ms_mean_max_rank": kern_ms_max,
                          "kernel": vec.kernel_name(),
+                         "grid": int(vec.launch_info.blocks) if vec.persistent else e,
                          "timing": "HIP events on the launch stream around each step"},
             "env_done_fraction_last_step": done_frac,
         }

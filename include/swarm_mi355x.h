@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SWARM_ABI_VERSION 2
+#define SWARM_ABI_VERSION 3
 
 /* error codes */
 #define SWARM_OK 0
@@ -58,7 +58,11 @@ extern "C" {
 
 /* kernel actually launched (swarm_launch_info_t.kernel_id) */
 #define SWARM_KERNEL_GENERIC 0  /* swarm_kernel<KIND, DYN, KS, MSL, LM> */
-#define SWARM_KERNEL_STEP64 1   /* swarm_step64: N = 64, K = 3, Ms = 4, 4 <= M <= 16, kinematic step */
+#define SWARM_KERNEL_STEP64 1   /* swarm_step64_once: N = 64, K = 3, Ms = 4, 4 <= M <= 16, kinematic step;
+                                   one wave per env, 4 envs per workgroup */
+#define SWARM_KERNEL_STEP64_PERSISTENT 2  /* swarm_step64: the same step on a persistent grid of
+                                   waves_per_simd waves per SIMD with per-XCD env queues
+                                   (E > grid; needs state.work, else STEP64 is launched) */
 
 /* env_done bits ([E] u8) */
 #define SWARM_ENV_TERMINATED 1u  /* terminated["__all__"] */
@@ -110,7 +114,7 @@ typedef struct swarm_params {
   double drone_contact_radius;    /* contact approximation radius of the 0.3x0.3x0.05 box */
   double ground_contact_height;   /* z at or below which the box touches the plane */
   int32_t kernel_path;       /* SWARM_PATH_* (default AUTO) */
-  int32_t reserved0;         /* must be 0 */
+  int32_t waves_per_simd;    /* persistent swarm_step64 grid: resident waves per SIMD (0 = library default) */
 } swarm_params_t;
 
 /* Per-env state, device SoA blocks (all dense, C-contiguous). */
@@ -123,7 +127,12 @@ typedef struct swarm_state {
   int32_t* step_count; /* [E] */
   uint32_t* episode;   /* [E]  device-RNG episode counter (incremented by every device reset) */
   float* damping;      /* [E,N] physics linear damping (NULL allowed in kinematic mode) */
+  uint32_t* work;      /* [SWARM_WORK_WORDS] env-queue heads of the persistent swarm_step64: zeroed
+                          once by the caller, left zeroed by every call; NULL = one workgroup per
+                          env.  Belongs to this state: concurrent calls need distinct buffers. */
 } swarm_state_t;
+
+#define SWARM_WORK_WORDS 256  /* 8 dequeue heads (one per XCD), one 128-B line each */
 
 /* Outputs.  Optional pointers may be NULL. */
 typedef struct swarm_out {

@@ -31,6 +31,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
+
 #include "swarm_mi355x.h"
 
 #pragma clang fp contract(off)
@@ -55,21 +57,25 @@
 #define ABL_RESET 8    // never auto-reset
 #define ABL_OBST 16    // skip the obstacle pass
 #define ABL_W64 64     // one-team waves use the generic (rolled) pair pass
+#define ABL_STORE_ONLY 128  // step64: obs stores straight from registers (wrong values)
+#define ABL_STAGE_ONLY 256  // step64: obs staged through LDS, not stored
+#define ABL_ROW_ONLY 512    // step64: obs row computed, neither staged nor stored
 
 // Diagnostic phase timestamps (tools/stamps.py; never set in the product build)
 #ifdef SWARM_STAMPS
 __device__ unsigned long long g_stamps[1 << 20];
-#define STAMP(i)                                                                         \
+#define STAMP_AT(rec, i)                                                                 \
   do {                                                                                   \
     __builtin_amdgcn_sched_barrier(0);                                                   \
     unsigned long long ts_;                                                              \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");           \
     __builtin_amdgcn_sched_barrier(0);                                                   \
-    if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) g_stamps[blockIdx.x * 16 + (i)] = ts_; \
+    if (threadIdx.x == 0 && (rec) < (1 << 16)) g_stamps[(rec) * 16 + (i)] = ts_;           \
   } while (0)
 #else
-#define STAMP(i) do {} while (0)
+#define STAMP_AT(rec, i) do {} while (0)
 #endif
+#define STAMP(i) STAMP_AT(blockIdx.x, i)
 
 namespace {
 
@@ -99,7 +105,7 @@ struct KParams {
   long long env_offset;
   unsigned seed_lo, seed_hi;
   float half_w, neg_half_w, width_w;
-  float dt, vmax, amax, ds_f;
+  float dt, vmax, amax, ds_f, s_vmax;  // s_vmax: largest s with sqrt_rn(s) <= vmax
   float thr_pair, s_pair, s_obst;   // kinematic: distance threshold, squared-space thresholds
   float thr_ppair, s_phys_pair, s_phys_obst, ground_z;
   float h, g, gcomp;
@@ -109,7 +115,17 @@ struct KParams {
 // ------------------------------------------------------------------ exact numerics
 // Correctly rounded square roots.  NB: HIP's __fsqrt_rn is v_sqrt_f32 (1 ulp) unless
 // OCML_BASIC_ROUNDED_OPERATIONS is defined; llvm.sqrt lowers to the IEEE-exact sequence.
-__device__ __forceinline__ float sqrt_rn(float x) { return __builtin_sqrtf(x); }
+// The fast path is OCML's own correction step without its input scaling (needed only below
+// 2^-96) and special-value fixup (inf/NaN/negative never occur here): bit-identical results.
+__device__ __forceinline__ float sqrt_rn(float x) {
+  if (__builtin_expect(__ballot(!(x >= 0x1p-96f || x == 0.0f)) != 0, 0)) return __builtin_sqrtf(x);
+  float r = __builtin_amdgcn_sqrtf(x);  // v_sqrt_f32, within 1 ulp
+  const float rm = __uint_as_float(__float_as_uint(r) - 1u), rp = __uint_as_float(__float_as_uint(r) + 1u);
+  const float em = __builtin_fmaf(-rm, r, x), ep = __builtin_fmaf(-rp, r, x);
+  r = (em <= 0.0f) ? rm : r;
+  r = (ep > 0.0f) ? rp : r;
+  return r;
+}
 __device__ __forceinline__ double dsqrt_rn(double x) { return __builtin_sqrt(x); }
 // np.linalg.norm(v) of a float32 3-vector: OpenBLAS sdot = double accumulation of float
 // products, rounded to float.  Returns the float sum s; the norm is sqrt_rn(s).
@@ -120,11 +136,17 @@ __device__ __forceinline__ float sqsum_1d(float x, float y, float z) {
 // np.linalg.norm(A, axis=1): float32 ((x*x)+(y*y))+(z*z).  Also the ranking value s'.
 __device__ __forceinline__ float sqsum_f(float x, float y, float z) { return ((x * x) + (y * y)) + (z * z); }
 
+// np.clip of a float32 in [lo, hi] (lo <= hi): one v_med3_f32
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
 __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t r;
   asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
+// 1/n for the formation mean (np.mean over the n_active - 1 partner terms): v_rcp_f32 (1 ulp)
+// instead of an f64 division; the mean is then within ~1e-7 relative, inside the 1e-5 reward
+// contract (the terms themselves carry d~ = v_sqrt_f32 distances).
+__device__ __forceinline__ double inv_count(int n) { return (double)__builtin_amdgcn_rcpf((float)n); }
 // Insert key into the ascending list k[0..S-1] (drops the largest): one med3 per slot.
 template <int S>
 __device__ __forceinline__ void kins(uint32_t (&k)[S], uint32_t key) {
@@ -152,6 +174,14 @@ __device__ __forceinline__ void philox4x32_10(uint32_t (&c)[4], uint32_t k0, uin
 __device__ __forceinline__ float uni(uint32_t x, float lo, float width) {
   const float u = (float)(x >> 8) * 0x1p-24f;
   return lo + u * width;
+}
+__device__ __forceinline__ void draw_block_k(uint32_t k0, uint32_t k1, long long genv, uint32_t episode,
+                                             uint32_t block, uint32_t (&w)[4]) {
+  w[0] = block;
+  w[1] = episode;
+  w[2] = (uint32_t)((unsigned long long)genv & 0xffffffffull);
+  w[3] = (uint32_t)((unsigned long long)genv >> 32);
+  philox4x32_10(w, k0, k1);
 }
 __device__ __forceinline__ void draw_block(const KParams& P, long long genv, uint32_t episode,
                                            uint32_t block, uint32_t (&w)[4]) {
@@ -261,7 +291,50 @@ __device__ __forceinline__ void pair_pass_wave(const float4* __restrict__ ring, 
 }
 
 // One team per wave (L = 64): fully unrolled, every LDS / ds_bpermute address is the lane's
-// base plus an immediate offset (ds_bpermute takes the source lane modulo 64).
+// base plus an immediate offset (ds_bpermute takes the source lane modulo 64).  Rotations are
+// processed in groups of NB (ring reads, distances, ds_bpermutes of a group in flight together);
+// the formation terms of a group are summed in f32, then added to the f64 accumulator.
+#ifndef SWARM_PAIR_BATCH
+#define SWARM_PAIR_BATCH 4
+#endif
+template <int KS, int PASS, bool FAST, int R, int NB, bool MIRROR>
+__device__ __forceinline__ void pair_group_w64(const float4* __restrict__ q0, uint32_t t4, float px, float py, float pz,
+                                               bool self, uint32_t sflag, uint32_t keep, uint32_t keep_m, float ds,
+                                               uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum) {
+  float4 q[NB];
+  float sq[NB];
+  uint32_t v[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) q[i] = q0[R + i];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) sq[i] = sqsum_f(q[i].x - px, q[i].y - py, q[i].z - pz);
+  float esum = 0.f;
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+    v[i] = own_pair<KS, PASS, FAST>(nk, sq[i], (uint32_t)(R + i), self & (q[i].w != 0.f), keep, ds, smin, esum);
+  if constexpr (MIRROR) {
+    uint32_t rc[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      rc[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t4 + (uint32_t)(256 - 4 * (R + i))), (int)(v[i] | sflag));
+#pragma unroll
+    for (int i = 0; i < NB; ++i) mirror_pair<KS, PASS, FAST>(nk, rc[i], (uint32_t)(64 - R - i), self, keep_m, ds, smin, esum);
+  }
+  if constexpr (PASS == 1) fsum += (double)esum;
+}
+template <int KS, int PASS, bool FAST, int R, int B>
+__device__ __forceinline__ void pair_groups_w64(const float4* __restrict__ q0, uint32_t t4, float px, float py, float pz,
+                                                bool self, uint32_t sflag, uint32_t keep, uint32_t keep_m, float ds,
+                                                uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum) {
+  // rotations R .. 31 carry a mirror; rotation 32 pairs t with t+32 from both sides (own only)
+  if constexpr (R <= 31) {
+    constexpr int NB = (31 - R + 1) < B ? (31 - R + 1) : B;
+    pair_group_w64<KS, PASS, FAST, R, NB, true>(q0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum);
+    pair_groups_w64<KS, PASS, FAST, R + NB, B>(q0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum);
+  } else {
+    pair_group_w64<KS, PASS, FAST, 32, 1, false>(q0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum);
+  }
+}
 template <int KS, int PASS, bool FAST>
 __device__ __forceinline__ void pair_pass_w64(const float4* __restrict__ ring, int t, float px, float py, float pz,
                                               bool self, uint32_t keep, float ds, uint32_t (&nk)[KS > 0 ? KS : 1],
@@ -269,35 +342,8 @@ __device__ __forceinline__ void pair_pass_w64(const float4* __restrict__ ring, i
   const uint32_t sflag = (FAST || self) ? 0u : 0x80000000u;
   const uint32_t keep_m = keep & 0x7fffffffu;
   const uint32_t t4 = (uint32_t)t << 2;
-  const float4* q0 = ring + t;
-#pragma unroll
-  for (int r = 1; r < 31; r += 2) {
-    const float4 qa = q0[r];
-    const float4 qb = q0[r + 1];
-    const float sa = sqsum_f(qa.x - px, qa.y - py, qa.z - pz);
-    const float sb = sqsum_f(qb.x - px, qb.y - py, qb.z - pz);
-    float esum = 0.f;
-    const uint32_t va = own_pair<KS, PASS, FAST>(nk, sa, (uint32_t)r, self && (qa.w != 0.f), keep, ds, smin, esum);
-    const uint32_t vb = own_pair<KS, PASS, FAST>(nk, sb, (uint32_t)(r + 1), self && (qb.w != 0.f), keep, ds, smin, esum);
-    const uint32_t ra = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t4 + (uint32_t)(256 - 4 * r)), (int)(va | sflag));
-    const uint32_t rb =
-        (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t4 + (uint32_t)(256 - 4 * (r + 1))), (int)(vb | sflag));
-    mirror_pair<KS, PASS, FAST>(nk, ra, (uint32_t)(64 - r), self, keep_m, ds, smin, esum);
-    mirror_pair<KS, PASS, FAST>(nk, rb, (uint32_t)(64 - r - 1), self, keep_m, ds, smin, esum);
-    if constexpr (PASS == 1) fsum += (double)esum;
-  }
-  float esum = 0.f;
-  {  // r = 31: last rotation with a mirror
-    const float4 qa = q0[31];
-    const float sa = sqsum_f(qa.x - px, qa.y - py, qa.z - pz);
-    const uint32_t va = own_pair<KS, PASS, FAST>(nk, sa, 31u, self && (qa.w != 0.f), keep, ds, smin, esum);
-    const uint32_t ra = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t4 + (uint32_t)(256 - 4 * 31)), (int)(va | sflag));
-    mirror_pair<KS, PASS, FAST>(nk, ra, 33u, self, keep_m, ds, smin, esum);
-  }
-  const float4 qh = q0[32];
-  const float sh = sqsum_f(qh.x - px, qh.y - py, qh.z - pz);
-  own_pair<KS, PASS, FAST>(nk, sh, 32u, self && (qh.w != 0.f), keep, ds, smin, esum);
-  if constexpr (PASS == 1) fsum += (double)esum;
+  pair_groups_w64<KS, PASS, FAST, 1, SWARM_PAIR_BATCH>(ring + t, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin,
+                                                       fsum);
 }
 
 template <int KS, int PASS>
@@ -381,8 +427,12 @@ __device__ __forceinline__ bool finish_keys(const uint32_t (&k)[S], const float4
   if (last == KEY_EMPTY || ((((int)(last & imask) + ibase) & imod) >= count)) return true;
   if (K <= 0) return true;
   const float base = __uint_as_float(last & keep);
-  const float dlb = APPROX ? (dkey ? base * FAST_LO : sqrt_rn(base * FAST_LO)) : sqrt_rn(base);
-  return dlb > wd[K - 1];
+  const float w = wd[K - 1];
+  if (APPROX && dkey) return base * FAST_LO > w;
+  // squared space (no sqrt): base(1 - 2^-18) > w^2 (1 + 2^-18) in f32 implies every
+  // non-survivor's exact distance exceeds w strictly (keys are within 2^-21 of exact s; key
+  // truncation only lowers base); a near-equality falls to exact_select, which is exact anyway
+  return (APPROX ? base * FAST_LO : base) > (w * w) * FAST_HI;
 }
 
 // Largest of the first K entries of a register array (= entry K-1 of a sorted list), as a
@@ -527,26 +577,29 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       if (act) {  // drone_swarm_env.py:98-111
         prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
         if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
-        ax = fminf(fmaxf(ax, -1.f), 1.f) * P.amax;
-        ay = fminf(fmaxf(ay, -1.f), 1.f) * P.amax;
-        az = fminf(fmaxf(az, -1.f), 1.f) * P.amax;
+        ax = clampf(ax, -1.f, 1.f) * P.amax;
+        ay = clampf(ay, -1.f, 1.f) * P.amax;
+        az = clampf(az, -1.f, 1.f) * P.amax;
         vx = vx + ax * P.dt;
         vy = vy + ay * P.dt;
         vz = vz + az * P.dt;
-        const float sp = sqrt_rn(sqsum_1d(vx, vy, vz));  // _clip_speed :179-183
-        if (!(sp <= P.vmax || sp < (float)1e-8)) {
-          vx = (vx / sp) * P.vmax;
-          vy = (vy / sp) * P.vmax;
-          vz = (vz / sp) * P.vmax;
+        const float s_sp = sqsum_1d(vx, vy, vz);  // _clip_speed :179-183
+        if (!(s_sp <= P.s_vmax)) {
+          const float sp = sqrt_rn(s_sp);
+          if (!(sp <= P.vmax || sp < (float)1e-8)) {
+            vx = (vx / sp) * P.vmax;
+            vy = (vy / sp) * P.vmax;
+            vz = (vz / sp) * P.vmax;
+          }
         }
         px = px + vx * P.dt;
         py = py + vy * P.dt;
         pz = pz + vz * P.dt;
       }
       if (n_active > 0) {  // world clip of ALL drones, :113-117
-        px = fminf(fmaxf(px, P.neg_half_w), P.half_w);
-        py = fminf(fmaxf(py, P.neg_half_w), P.half_w);
-        pz = fminf(fmaxf(pz, P.neg_half_w), P.half_w);
+        px = clampf(px, P.neg_half_w, P.half_w);
+        py = clampf(py, P.neg_half_w, P.half_w);
+        pz = clampf(pz, P.neg_half_w, P.half_w);
       }
     } else {
       // point-mass restatement of drone_physics_env.py:323-360
@@ -729,7 +782,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
           p_coll = collided;
           p_cand = !reached && !collided;
           double r = ((double)prev_d - (double)curr) * P.kp;
-          if (n_active > 1) r = r + (-P.kf) * (fsum / (double)(n_active - 1));
+          if (n_active > 1) r = r + (-P.kf) * (fsum * inv_count(n_active - 1));
           if (reached) r = r + P.r_goal;
           if (collided) r = r + P.r_col;
           rew = (float)r;
@@ -1017,78 +1070,152 @@ constexpr int S64_D = 9 + 4 * S64_K + 4 * S64_MS;  // 37
 constexpr int S64_MMAX = 16;
 constexpr int S64_RING = 96;
 constexpr int S64_CH = 16;  // obs rows per LDS staging chunk (multiple of 4: 16-B aligned chunks)
+constexpr int S64_HEADS = 8;  // env-queue heads, one per XCD (blockIdx mod 8)
+constexpr int S64_HEAD_STRIDE = SWARM_WORK_WORDS / S64_HEADS;  // one 128-B line per head
+constexpr int S64_WPS_DEFAULT = 8;  // persistent grid: waves per SIMD (8: one wave per env up to E = 8 x 4 x CUs)
+constexpr int S64_MIN_WAVES = 6;    // register budget of swarm_step64 (<= 80 VGPRs)
 
-template <int CH>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
-swarm_step64(const KParams P, const swarm_state_t S, const float* __restrict__ actions,
-             const uint8_t* __restrict__ amask, const swarm_out_t O) {
+// LDS ordering inside one wave: every LDS region of the step64 body belongs to one wave, whose
+// LDS instructions execute in issue order, so a compiler fence is all that is needed (several
+// envs share a workgroup without coupling their waves through s_barrier).
+#ifndef SWARM_PRIO_MODE
+#define SWARM_PRIO_MODE 0
+#endif
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One env's inputs, loaded one env ahead of its compute (software pipeline): raw loaded values
+// only — any arithmetic on them here would make the wave wait for the loads right away.
+struct S64In {
+  float px, py, pz, vx, vy, vz, ax, ay, az;  // lane t = drone t
+  float ox, oy, oz;                          // lanes t < M: obstacle t
+  uint32_t act, has;                         // raw bytes of active / action_mask
+  uint32_t gse;  // lanes 0-2: goal x, y, z bits; lane 3: step count; lane 4: episode counter
+};
+
+// The kernel's only argument.  The body re-reads the fields it needs from the kernarg segment
+// phase by phase (s64_args: an opaque copy of the kernarg pointer, so the compiler cannot keep
+// the ~40 loop-invariant parameters and pointers live in SGPRs across the persistent loop and
+// spill them; scalar-cache hits cost a few cycles).
+struct S64Args {
+  KParams P;
+  swarm_state_t S;
+  const float* actions;
+  const uint8_t* amask;
+  swarm_out_t O;
+};
+#define KARG __attribute__((address_space(4)))
+typedef const KARG S64Args* S64ArgPtr;
+__device__ __forceinline__ S64ArgPtr s64_args() {
+  uint64_t v = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+  asm volatile("" : "+s"(v));
+  return reinterpret_cast<S64ArgPtr>(v);
+}
+
+__device__ __forceinline__ void s64_load(S64ArgPtr A, int env, int t, S64In& c) {
+  const float* __restrict__ actions = A->actions;
+  const uint8_t* __restrict__ amask = A->amask;
+  const size_t ea = (size_t)env * S64_N;
+  const unsigned t3 = 3u * (unsigned)t;
+  const float* __restrict__ pe = A->S.pos + ea * 3;
+  const float* __restrict__ ve = A->S.vel + ea * 3;
+  const float* __restrict__ ae = actions + ea * 3;
+  {  // env-uniform words, one per lane (a uniform load would be waited for at once)
+    const uint32_t* src = t < 3 ? reinterpret_cast<const uint32_t*>(A->S.goal) + 3 * env + t
+                                : (t == 3 ? reinterpret_cast<const uint32_t*>(A->S.step_count) + env : A->S.episode + env);
+    c.gse = 0u;
+    if (t < 5) c.gse = *src;
+  }
+  c.ax = ae[t3]; c.ay = ae[t3 + 1]; c.az = ae[t3 + 2];
+  c.px = pe[t3]; c.py = pe[t3 + 1]; c.pz = pe[t3 + 2];
+  c.vx = ve[t3]; c.vy = ve[t3 + 1]; c.vz = ve[t3 + 2];
+  // unconditional loads (no phi with a default value: that would need the data at once)
+  c.act = (A->S.active + ea)[t];
+  c.has = (amask != nullptr ? amask : A->S.active)[ea + t];  // without a mask: ignored by the body
+  const int m = t < A->P.M ? t : A->P.M - 1;  // lanes >= M re-load the last obstacle (unused)
+  const float* __restrict__ o = A->S.obstacles + ((size_t)env * A->P.M + m) * 3;
+  c.ox = o[0]; c.oy = o[1]; c.oz = o[2];
+}
+
+// One env of the step (all phases) from its prefetched inputs.
+// `prefetch` runs once every input has been consumed (after the integrate phase): it may
+// overwrite `c` with the next env's inputs, whose loads then overlap the rest of this env.
+template <int CH, class Prefetch>
+__device__ __forceinline__ void s64_env(const int env, const int M, const S64In& c, float4* __restrict__ ring,
+                                        float4* __restrict__ obst, float* __restrict__ stage, const int lane,
+                                        Prefetch&& prefetch) {
   constexpr int KS = S64_K + 1, MSL = S64_MS + 1, D = S64_D;
   static_assert(CH % 4 == 0 && S64_N % CH == 0, "chunk rows");
-  __shared__ float4 ring[S64_RING];
-  __shared__ float4 obst[S64_MMAX];
-  __shared__ __attribute__((aligned(16))) float stage[CH * D];
-  const int t = threadIdx.x;
-  const int env = blockIdx.x;
-  const int M = P.M;
+  // opaque copy of the lane index: keeps the ~40 lane-derived addresses and constants of the
+  // body (ds_bpermute sources, Philox products) from being hoisted out of the persistent loop,
+  // where they would be live across the whole body and spill
+  int t = lane;
+  asm volatile("" : "+v"(t));
   const unsigned t3 = 3u * (unsigned)t;
   const size_t ea = (size_t)env * S64_N;  // first agent of the env (uniform)
-  float* __restrict__ posE = S.pos + ea * 3;
-  float* __restrict__ velE = S.vel + ea * 3;
-  const float* __restrict__ actE = actions + ea * 3;
-  STAMP(0);
+  S64ArgPtr A = s64_args();  // re-fetched at every phase boundary
+  STAMP_AT(env, 0);
 #ifdef SWARM_STAMPS
-  if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) g_stamps[blockIdx.x * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0 && env < (1 << 16)) g_stamps[env * 16 + 11] = __builtin_amdgcn_s_memrealtime();
 #endif
 
-  // ---- load: env-uniform scalars, per-lane rows, obstacles to LDS
-  float gx = S.goal[3 * env + 0], gy = S.goal[3 * env + 1], gz = S.goal[3 * env + 2];
-  const int stepc = S.step_count[env];
-  const uint32_t episode0 = S.episode[env];
-  float ax = actE[t3], ay = actE[t3 + 1], az = actE[t3 + 2];
-  const bool has = (amask == nullptr) || ((amask + ea)[t] != 0);
-  float px = posE[t3], py = posE[t3 + 1], pz = posE[t3 + 2];
-  float vx = velE[t3], vy = velE[t3 + 1], vz = velE[t3 + 2];
-  bool act = (S.active + ea)[t] != 0;
-  if (t < M) {
-    const float* o = S.obstacles + ((size_t)env * M) * 3 + t3;
-    obst[t] = make_float4(o[0], o[1], o[2], 0.f);
-  }
+  // ---- inputs (prefetched): env-uniform scalars, per-lane rows, obstacles to LDS
+  float gx = __uint_as_float(__builtin_amdgcn_readlane(c.gse, 0));
+  float gy = __uint_as_float(__builtin_amdgcn_readlane(c.gse, 1));
+  float gz = __uint_as_float(__builtin_amdgcn_readlane(c.gse, 2));
+  const int stepc = (int)__builtin_amdgcn_readlane(c.gse, 3);
+  const uint32_t episode0 = (uint32_t)__builtin_amdgcn_readlane(c.gse, 4);
+  float ax = c.ax, ay = c.ay, az = c.az;
+  const bool has = s64_args()->amask == nullptr || c.has != 0;
+  float px = c.px, py = c.py, pz = c.pz;
+  float vx = c.vx, vy = c.vy, vz = c.vz;
+  bool act = c.act != 0;
+  if (t < M) obst[t] = make_float4(c.ox, c.oy, c.oz, 0.f);
   const int n_active = __popcll(__ballot(act));
-  STAMP(1);
+  STAMP_AT(env, 1);
 
   // ---- integrate: drone_swarm_env.py:98-117 (identical to swarm_kernel, DYN_KIN)
   float prev_d = 0.f;
   if (act) {
     prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
     if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
-    ax = fminf(fmaxf(ax, -1.f), 1.f) * P.amax;
-    ay = fminf(fmaxf(ay, -1.f), 1.f) * P.amax;
-    az = fminf(fmaxf(az, -1.f), 1.f) * P.amax;
-    vx = vx + ax * P.dt;
-    vy = vy + ay * P.dt;
-    vz = vz + az * P.dt;
-    const float sp = sqrt_rn(sqsum_1d(vx, vy, vz));
-    if (!(sp <= P.vmax || sp < (float)1e-8)) {
-      vx = (vx / sp) * P.vmax;
-      vy = (vy / sp) * P.vmax;
-      vz = (vz / sp) * P.vmax;
+    ax = clampf(ax, -1.f, 1.f) * A->P.amax;
+    ay = clampf(ay, -1.f, 1.f) * A->P.amax;
+    az = clampf(az, -1.f, 1.f) * A->P.amax;
+    vx = vx + ax * A->P.dt;
+    vy = vy + ay * A->P.dt;
+    vz = vz + az * A->P.dt;
+    const float s_sp = sqsum_1d(vx, vy, vz);
+    if (!(s_sp <= A->P.s_vmax)) {  // sqrt_rn(s_sp) <= vmax otherwise: the speed is needed only here
+      const float sp = sqrt_rn(s_sp);
+      if (!(sp <= A->P.vmax || sp < (float)1e-8)) {
+        vx = (vx / sp) * A->P.vmax;
+        vy = (vy / sp) * A->P.vmax;
+        vz = (vz / sp) * A->P.vmax;
+      }
     }
-    px = px + vx * P.dt;
-    py = py + vy * P.dt;
-    pz = pz + vz * P.dt;
+    px = px + vx * A->P.dt;
+    py = py + vy * A->P.dt;
+    pz = pz + vz * A->P.dt;
   }
   if (n_active > 0) {
-    px = fminf(fmaxf(px, P.neg_half_w), P.half_w);
-    py = fminf(fmaxf(py, P.neg_half_w), P.half_w);
-    pz = fminf(fmaxf(pz, P.neg_half_w), P.half_w);
+    px = clampf(px, A->P.neg_half_w, A->P.half_w);
+    py = clampf(py, A->P.neg_half_w, A->P.half_w);
+    pz = clampf(pz, A->P.neg_half_w, A->P.half_w);
   }
   {
     const float4 me = make_float4(px, py, pz, act ? 1.f : 0.f);
     ring[t] = me;
     if (t < S64_RING - S64_N) ring[t + S64_N] = me;
   }
-  __syncthreads();
-  STAMP(2);
+  wave_sync();
+  prefetch();  // `c` is dead from here on
+  if constexpr (SWARM_PRIO_MODE >= 2) __builtin_amdgcn_s_setprio(1);
+  STAMP_AT(env, 2);
+  A = s64_args();
 
   // ---- pair + obstacle passes
   uint32_t nk[KS], ok[MSL];
@@ -1100,44 +1227,60 @@ swarm_step64(const KParams P, const swarm_state_t S, const float* __restrict__ a
   float smin = __builtin_inff();
   double fsum = 0.0;
   const bool fast = __all(act);
-  if (fast) pair_pass_w64<KS, 1, true>(ring, t, px, py, pz, true, P.nb_keep, P.ds_f, nk, smin, fsum);
-  else pair_pass_w64<KS, 1, false>(ring, t, px, py, pz, act, P.nb_keep, P.ds_f, nk, smin, fsum);
-  obstacle_pass<MSL, true>(obst, M, px, py, pz, act, P.s_obst, P.ob_keep, ok, ocoll);
-  STAMP(3);
+#if SWARM_DIAG_EXTRA_VALU
+  {  // diagnostic: SWARM_DIAG_EXTRA_VALU dependent-free FAST VALU ops per wave
+    float z0 = px, z1 = py, z2 = pz, z3 = px + 1.f;
+#pragma unroll
+    for (int i = 0; i < SWARM_DIAG_EXTRA_VALU / 4; ++i) {
+      z0 = z0 * 0.999f; z1 = z1 * 0.999f; z2 = z2 * 0.999f; z3 = z3 * 0.999f;
+    }
+    if (z0 + z1 + z2 + z3 == 1234.5f) fsum += 1.0;
+  }
+#endif
+#if SWARM_DIAG_NO_FORMATION
+  if (fast) pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
+#else
+  if (fast) pair_pass_w64<KS, 1, true>(ring, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
+#endif
+  else pair_pass_w64<KS, 1, false>(ring, t, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
+  obstacle_pass<MSL, true>(obst, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
+  STAMP_AT(env, 3);
+  A = s64_args();
 
   // ---- exact top-K (finish_keys, rare exact_select)
   float wd[KS], od[MSL];
   int wj[KS], oj[MSL];
   auto select_topk = [&](bool dkey) {
-    const bool slow_nb = !finish_keys<KS, false, true>(nk, ring, S64_N, t, S64_N - 1, S64_K, P.nb_keep, dkey, px, py,
+    const bool slow_nb = !finish_keys<KS, false, true>(nk, ring, S64_N, t, S64_N - 1, S64_K, A->P.nb_keep, dkey, px, py,
                                                        pz, wd, wj);
-    const bool slow_ob = !finish_keys<MSL, true, false>(ok, obst, M, 0, 0x7fffffff, S64_MS, P.ob_keep, false, px, py,
+    const bool slow_ob = !finish_keys<MSL, true, false>(ok, obst, M, 0, 0x7fffffff, S64_MS, A->P.ob_keep, false, px, py,
                                                         pz, od, oj);
     if (slow_nb) exact_select<KS, false>(ring, S64_N, t, S64_K, max_first(wd, S64_K), px, py, pz, wd, wj);
     if (slow_ob) exact_select<MSL, true>(obst, M, -1, S64_MS, max_first(od, S64_MS), px, py, pz, od, oj);
   };
   select_topk(true);
-  STAMP(4);
+  STAMP_AT(env, 4);
+  A = s64_args();
 
   // ---- rewards / terminations: drone_swarm_env.py:120-172
   bool pcoll;
   if (fast) {
-    pcoll = wd[0] <= P.thr_pair;
+    pcoll = wd[0] <= A->P.thr_pair;
   } else {
-    pcoll = smin <= P.thr_pair * FAST_LO;
-    if (!pcoll && smin <= P.thr_pair * FAST_HI && act)
-      pcoll = exact_pair_collision(ring, S64_N, t, px, py, pz, P.s_pair);
+    pcoll = smin <= A->P.thr_pair * FAST_LO;
+    if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act)
+      pcoll = exact_pair_collision(ring, S64_N, t, px, py, pz, A->P.s_pair);
   }
   const float curr = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
   float rew = 0.f;
   bool reached = false, collided = false;
   if (act) {
-    reached = (double)curr <= P.goal_radius;
+    reached = (double)curr <= A->P.goal_radius;
     collided = ocoll || pcoll;
-    double r = ((double)prev_d - (double)curr) * P.kp;
-    if (n_active > 1) r = r + (-P.kf) * (fsum / (double)(n_active - 1));
-    if (reached) r = r + P.r_goal;
-    if (collided) r = r + P.r_col;
+    double r = ((double)prev_d - (double)curr) * A->P.kp;
+    if (n_active > 1) r = r + (-A->P.kf) * (fsum * inv_count(n_active - 1));
+    if (reached) r = r + A->P.r_goal;
+    if (collided) r = r + A->P.r_col;
     rew = (float)r;
   }
   const bool any_c = __ballot(act && collided) != 0;
@@ -1148,7 +1291,7 @@ swarm_step64(const KParams P, const swarm_state_t S, const float* __restrict__ a
     term_all = true;
   } else {
     new_step = stepc + 1;
-    const bool tl = new_step >= P.max_steps;
+    const bool tl = new_step >= A->P.max_steps;
     term_all = (!any_cand && !any_c && !tl) || any_c;
     trunc_all = tl && !term_all;
     if (act) {
@@ -1158,45 +1301,47 @@ swarm_step64(const KParams P, const swarm_state_t S, const float* __restrict__ a
       cont = !done_i && !tl && !any_c;
     }
   }
-  const bool do_reset = P.auto_reset && (term_all || trunc_all) && !(SWARM_ABLATE & ABL_RESET);
-  (O.reward + ea)[t] = rew;
-  if (O.dist_goal) (O.dist_goal + ea)[t] = curr;
-  if (O.info_flags)
-    (O.info_flags + ea)[t] = (uint8_t)((act ? SWARM_AGENT_STEPPED : 0u) | (act && reached ? SWARM_AGENT_REACHED : 0u) |
+  const bool do_reset = A->P.auto_reset && (term_all || trunc_all) && !(SWARM_ABLATE & ABL_RESET);
+  (A->O.reward + ea)[t] = rew;
+  if (A->O.dist_goal) (A->O.dist_goal + ea)[t] = curr;
+  if (A->O.info_flags)
+    (A->O.info_flags + ea)[t] = (uint8_t)((act ? SWARM_AGENT_STEPPED : 0u) | (act && reached ? SWARM_AGENT_REACHED : 0u) |
                                        (act && collided ? SWARM_AGENT_COLLISION : 0u) |
                                        (cont ? SWARM_AGENT_HAS_OBS : 0u));
   if (t == 0)
-    O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
+    A->O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
                                 (do_reset ? SWARM_ENV_RESET : 0u));
   const uint64_t m_term = __ballot(term), m_trunc = __ballot(trunc);
-  STAMP(5);
+  STAMP_AT(env, 5);
+  A = s64_args();
 
   // ---- in-kernel auto-reset (wave-uniform): new episode, then its key passes
   uint32_t episode_new = episode0;
   if (do_reset) {
-    const long long genv = P.env_offset + env;
+    if constexpr (SWARM_PRIO_MODE >= 1) __builtin_amdgcn_s_setprio(3);  // longest remaining work first
+    const long long genv = A->P.env_offset + env;
     episode_new = episode0 + 1u;
-    uint32_t w[4];
-    draw_block(P, genv, episode_new, (uint32_t)t, w);
-    px = uni(w[0], P.neg_half_w, P.width_w);
-    py = uni(w[1], P.neg_half_w, P.width_w);
-    pz = uni(w[2], P.neg_half_w, P.width_w);
+    // two independent Philox chains per lane: drone t (block t), and obstacle t (block N + t) for
+    // lanes t < M / the goal (block N + M) on lane M
+    uint32_t w[4], wo[4];
+    draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)t, w);
+    draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)(S64_N + (t < M ? t : M)), wo);
+    const float lo_w = A->P.neg_half_w, wd_w = A->P.width_w;
+    px = uni(w[0], lo_w, wd_w);
+    py = uni(w[1], lo_w, wd_w);
+    pz = uni(w[2], lo_w, wd_w);
     vx = vy = vz = 0.f;
     act = true;
-    __syncthreads();  // every read of the old ring / obstacles is done
-    if (t < M) {
-      draw_block(P, genv, episode_new, (uint32_t)(S64_N + t), w);
-      obst[t] = make_float4(uni(w[0], P.neg_half_w, P.width_w), uni(w[1], P.neg_half_w, P.width_w),
-                            uni(w[2], P.neg_half_w, P.width_w), 0.f);
-    }
-    draw_block(P, genv, episode_new, (uint32_t)(S64_N + M), w);
-    gx = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(uni(w[0], P.neg_half_w, P.width_w))));
-    gy = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(uni(w[1], P.neg_half_w, P.width_w))));
-    gz = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(uni(w[2], P.neg_half_w, P.width_w))));
+    const float ox = uni(wo[0], lo_w, wd_w), oy = uni(wo[1], lo_w, wd_w), oz = uni(wo[2], lo_w, wd_w);
+    wave_sync();  // every read of the old ring / obstacles is done
+    if (t < M) obst[t] = make_float4(ox, oy, oz, 0.f);
+    gx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ox), M));
+    gy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(oy), M));
+    gz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(oz), M));
     const float4 me = make_float4(px, py, pz, 1.f);
     ring[t] = me;
     if (t < S64_RING - S64_N) ring[t + S64_N] = me;
-    __syncthreads();
+    wave_sync();
 #pragma unroll
     for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
 #pragma unroll
@@ -1204,14 +1349,17 @@ swarm_step64(const KParams P, const swarm_state_t S, const float* __restrict__ a
     bool c2 = false;
     float s2 = 0.f;
     double f2 = 0.0;
-    pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
-    obstacle_pass<MSL, false>(obst, M, px, py, pz, false, 0.f, P.ob_keep, ok, c2);
+    pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, A->P.nb_keep, 0.f, nk, s2, f2);
+    obstacle_pass<MSL, false>(obst, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
     select_topk(false);
   }
 
-  STAMP(6);
+  STAMP_AT(env, 6);
+  A = s64_args();
   // ---- state write-back
   const bool new_act = do_reset || cont;
+  float* __restrict__ posE = A->S.pos + ea * 3;
+  float* __restrict__ velE = A->S.vel + ea * 3;
   posE[t3] = px; posE[t3 + 1] = py; posE[t3 + 2] = pz;
   velE[t3] = vx; velE[t3 + 1] = vy; velE[t3 + 2] = vz;
   {  // terminated, truncated, active: three 64-B rows of bytes built from wave ballots
@@ -1221,30 +1369,31 @@ swarm_step64(const KParams P, const swarm_state_t S, const float* __restrict__ a
       const uint64_t m = grp == 0 ? m_term : (grp == 1 ? m_trunc : m_act);
       const uint32_t nib = (uint32_t)(m >> (4 * (t & 15))) & 0xFu;
       const uint32_t word = (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
-      uint8_t* base = grp == 0 ? O.terminated : (grp == 1 ? O.truncated : S.active);
+      uint8_t* base = grp == 0 ? A->O.terminated : (grp == 1 ? A->O.truncated : A->S.active);
       *reinterpret_cast<uint32_t*>(base + ea + 4 * (t & 15)) = word;
     }
   }
   if (t == 0) {
-    S.step_count[env] = do_reset ? 0 : new_step;
+    A->S.step_count[env] = do_reset ? 0 : new_step;
     if (do_reset) {
-      S.episode[env] = episode_new;
-      S.goal[3 * env + 0] = gx; S.goal[3 * env + 1] = gy; S.goal[3 * env + 2] = gz;
+      A->S.episode[env] = episode_new;
+      A->S.goal[3 * env + 0] = gx; A->S.goal[3 * env + 1] = gy; A->S.goal[3 * env + 2] = gz;
     }
   }
   if (do_reset && t < M) {
-    float* o = S.obstacles + ((size_t)env * M) * 3 + t3;
+    float* o = A->S.obstacles + ((size_t)env * M) * 3 + t3;
     const float4 q = obst[t];
     o[0] = q.x; o[1] = q.y; o[2] = q.z;
   }
-  if (O.global_state) {
-    float* gs = O.global_state + (size_t)env * (6 * S64_N + 3);
+  if (A->O.global_state) {
+    float* gs = A->O.global_state + (size_t)env * (6 * S64_N + 3);
     gs[t3] = px; gs[t3 + 1] = py; gs[t3 + 2] = pz;
     gs[3 * S64_N + t3] = vx; gs[3 * S64_N + t3 + 1] = vy; gs[3 * S64_N + t3 + 2] = vz;
     if (t == 0) { gs[6 * S64_N + 0] = gx; gs[6 * S64_N + 1] = gy; gs[6 * S64_N + 2] = gz; }
   }
 
-  STAMP(7);
+  STAMP_AT(env, 7);
+  A = s64_args();
   // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)] (drone_swarm_env.py:226-291)
   float row[D];
   row[0] = px; row[1] = py; row[2] = pz;
@@ -1262,32 +1411,176 @@ swarm_step64(const KParams P, const swarm_state_t S, const float* __restrict__ a
   }
   if (SWARM_ABLATE & ABL_OBS) return;
   constexpr int V4 = CH * D / 4;  // float4 per chunk
-  float4* __restrict__ dst = reinterpret_cast<float4*>(O.obs + ea * D);
+  float4* __restrict__ dst = reinterpret_cast<float4*>(A->O.obs + ea * D);
+  if (SWARM_ABLATE & ABL_STORE_ONLY) {  // diagnostic: the obs stores without the LDS staging (wrong values)
+#pragma unroll
+    for (int ch = 0; ch < S64_N / CH; ++ch)
+#pragma unroll
+      for (int i = t; i < V4; i += 64) dst[ch * V4 + i] = make_float4(row[i & 7], row[9 + (i & 7)], row[18], row[30]);
+    return;
+  }
+  if (SWARM_ABLATE & ABL_ROW_ONLY) {  // diagnostic: the obs row computed, neither staged nor stored
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < D; ++i) acc += row[i];
+    if (acc == 12345.f) dst[t] = make_float4(acc, acc, acc, acc);
+    return;
+  }
+  if (SWARM_ABLATE & ABL_STAGE_ONLY) {  // diagnostic: the LDS staging without the obs stores
+    float acc = 0.f;
+    float* srow0 = stage + (t % CH) * D;
+#pragma unroll
+    for (int ch = 0; ch < S64_N / CH; ++ch) {
+      if (t / CH == ch) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) srow0[i] = row[i];
+      }
+      wave_sync();
+      const float4* s4 = reinterpret_cast<const float4*>(stage);
+#pragma unroll
+      for (int i = t; i < V4; i += 64) { const float4 q = s4[i]; acc += q.x + q.y + q.z + q.w; }
+      wave_sync();
+    }
+    if (acc == 12345.f) dst[t] = make_float4(acc, acc, acc, acc);
+    return;
+  }
   const float4* s4 = reinterpret_cast<const float4*>(stage);
   float* srow = stage + (t % CH) * D;
 #pragma unroll
-  for (int c = 0; c < S64_N / CH; ++c) {
-    if (t / CH == c) {
+  for (int ch = 0; ch < S64_N / CH; ++ch) {
+    if (t / CH == ch) {
 #pragma unroll
       for (int i = 0; i < D; ++i) srow[i] = row[i];
     }
-    __syncthreads();
+    wave_sync();
 #pragma unroll
-    for (int i = t; i < V4; i += 64) dst[c * V4 + i] = s4[i];
-    __syncthreads();
+    for (int i = t; i < V4; i += 64) dst[ch * V4 + i] = s4[i];
+    wave_sync();
   }
-  STAMP(8);
+  STAMP_AT(env, 8);
 #ifdef SWARM_STAMPS
-  if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) {
-    g_stamps[blockIdx.x * 16 + 9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
-    g_stamps[blockIdx.x * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-    g_stamps[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0 && env < (1 << 16)) {
+    g_stamps[env * 16 + 9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+    g_stamps[env * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    g_stamps[env * 16 + 12] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
 }
 
+// The kernel.  Without a work buffer (S.work == NULL): one env per workgroup.  With one: a
+// persistent grid of G workgroups (waves_per_simd resident per SIMD).  Workgroups with
+// blockIdx = x (mod H), H = min(8, G) — one XCD under the observed round-robin placement; that
+// is locality only, never correctness — share the env range [E*x/H, E*(x+1)/H) and the queue
+// head work[32x]: the k-th of them starts on env lo + k, every further env costs one returning
+// device-scope atomicAdd on the head.  Every workgroup draws until its first failing ticket, so
+// a launch draws exactly (envs beyond the first round) + (workgroups) tickets from each head, and
+// the workgroup that draws the last one resets the head to 0 (the next launch on the stream sees
+// it).  Envs are independent, so the env -> workgroup assignment never changes a result.
+// Software pipeline: once env i has consumed its inputs (after integrate), the inputs of env i+1
+// and the ticket of env i+2 are issued; they land while env i finishes, and env i's stores
+// drain while env i+1 computes.
+// Diagnostic: wave priority cohorts (s_setprio by blockIdx) to stagger when waves finish.
+#ifndef SWARM_PRIO_LEVELS
+#define SWARM_PRIO_LEVELS 0
+#endif
+#ifndef SWARM_PRIO_MODE
+#define SWARM_PRIO_MODE 0
+#endif
+__device__ __forceinline__ void s64_set_priority() {
+  if constexpr (SWARM_PRIO_LEVELS > 1) {
+    const int lvl = (int)((blockIdx.x >> 3) % SWARM_PRIO_LEVELS) * 3 / (SWARM_PRIO_LEVELS - 1);
+    switch (lvl) {
+      case 0: __builtin_amdgcn_s_setprio(3); break;
+      case 1: __builtin_amdgcn_s_setprio(2); break;
+      case 2: __builtin_amdgcn_s_setprio(1); break;
+      default: __builtin_amdgcn_s_setprio(0); break;
+    }
+  }
+}
+
+// One wave per env (the launch when the grid covers E): no loop, 8 waves per SIMD.  G envs per
+// workgroup of G independent waves: 8192 one-wave workgroups take the dispatcher ~4 us to start,
+// a quarter as many 4-wave ones about 1 us.
+#ifndef SWARM_S64_WG_ENVS
+#define SWARM_S64_WG_ENVS 4
+#endif
+constexpr int S64_WG_ENVS = SWARM_S64_WG_ENVS;
+template <int CH, int G>
+__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(8)))
+swarm_step64_once(const S64Args args) {
+  (void)args;  // read through s64_args()
+  __shared__ float4 ring[G][S64_RING];
+  __shared__ float4 obst[G][S64_MMAX];
+  __shared__ __attribute__((aligned(16))) float stage[G][CH * S64_D];
+  s64_set_priority();
+  if constexpr (SWARM_PRIO_MODE >= 2) __builtin_amdgcn_s_setprio(3);  // inputs and integrate first
+  const int t = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int env = blockIdx.x * G + w;
+  if (env >= s64_args()->P.E) return;  // whole wave (the last workgroup of a ragged E)
+  S64In cur;
+  s64_load(s64_args(), env, t, cur);
+  s64_env<CH>(env, s64_args()->P.M, cur, ring[w], obst[w], stage[w], t, []() {});
+}
+
+template <int CH>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(S64_MIN_WAVES)))
+swarm_step64(const S64Args args) {
+  (void)args;  // read through s64_args()
+  __shared__ float4 ring[S64_RING];
+  __shared__ float4 obst[S64_MMAX];
+  __shared__ __attribute__((aligned(16))) float stage[CH * S64_D];
+  const int t = threadIdx.x;
+  uint32_t* head = nullptr;
+  int env, base = 0;
+  uint32_t n_dyn = 0, n_draws = 0;
+  S64ArgPtr A = s64_args();
+  const int M = A->P.M;
+  if (A->S.work == nullptr) {
+    env = blockIdx.x;
+  } else {
+    const int G = gridDim.x;
+    const int H = G < S64_HEADS ? G : S64_HEADS;  // heads in use: every head has a workgroup
+    const int x = blockIdx.x % H, k = blockIdx.x / H;
+    const int lo = (int)(((long long)A->P.E * x) / H), hi = (int)(((long long)A->P.E * (x + 1)) / H);
+    const int gx = (G - x + H - 1) / H;  // workgroups on this head
+    const int n = hi - lo;
+    env = k < n ? lo + k : -1;
+    base = lo + gx;
+    n_dyn = n > gx ? (uint32_t)(n - gx) : 0u;
+    n_draws = n_dyn + (uint32_t)gx;
+    head = A->S.work + S64_HEAD_STRIDE * x;
+  }
+  auto draw = [&]() -> uint32_t {  // issue only: the value is consumed one env later
+    uint32_t v = 0xffffffffu;
+    if (head != nullptr && t == 0) v = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+  };
+  auto settle = [&](uint32_t v) -> int {
+    if (head == nullptr) return -1;
+    v = __builtin_amdgcn_readfirstlane(v);
+    if (v == n_draws - 1u && t == 0) __hip_atomic_store(head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v < n_dyn ? base + (int)v : -1;
+  };
+  S64In cur;
+  const bool first = env >= 0;
+  if (first) s64_load(A, env, t, cur);
+  uint32_t ticket = draw();
+  while (env >= 0) {
+    const int nxt = settle(ticket);
+    s64_env<CH>(env, M, cur, ring, obst, stage, t, [&]() {
+      if (nxt >= 0) {
+        s64_load(s64_args(), nxt, t, cur);
+        ticket = draw();
+      }
+    });
+    env = nxt;
+  }
+  if (!first) settle(ticket);
+}
+
 // ------------------------------------------------------------------ host side
-typedef void (*step64_fn)(const KParams, const swarm_state_t, const float*, const uint8_t*, const swarm_out_t);
+typedef void (*step64_fn)(const S64Args);
 typedef void (*kernel_fn)(const KParams, const swarm_state_t, const float*, const uint8_t*, const swarm_out_t,
                           const uint8_t*, int);
 
@@ -1333,9 +1626,12 @@ SWARM_PICK_DECL(1);
 SWARM_PICK_DECL(2);
 SWARM_PICK_DECL(3);
 // the headline specialisation (SWARM_PART 5)
-__attribute__((visibility("hidden"))) void* swarm_pick_step64();
+__attribute__((visibility("hidden"))) void* swarm_pick_step64(bool persistent);
 #if SWARM_HAS_PART(5)
-__attribute__((visibility("hidden"))) void* swarm_pick_step64() { return reinterpret_cast<void*>(swarm_step64<S64_CH>); }
+__attribute__((visibility("hidden"))) void* swarm_pick_step64(bool persistent) {
+  return persistent ? reinterpret_cast<void*>(swarm_step64<S64_CH>)
+                    : reinterpret_cast<void*>(swarm_step64_once<S64_CH, S64_WG_ENVS>);
+}
 #endif
 #if SWARM_HAS_PART(0)
 SWARM_PICK_DECL(0) { return pick_lm<KIND_STEP, DYN_KIN>(lm, ks, msl); }
@@ -1413,6 +1709,25 @@ bool step64_applies(const swarm_params_t* p, const KParams& k) {
          k.M <= S64_MMAX && p->dynamics == DYN_KIN;
 }
 
+// Persistent grid of swarm_step64: waves_per_simd x 4 SIMDs x the current device's CUs (E when
+// no device is visible, e.g. host-only queries).
+int step64_grid(const swarm_params_t* p, int E) {
+  static std::atomic<int> cu_cache[64];
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return E;
+  if (dev < 64) cus = cu_cache[dev].load(std::memory_order_relaxed);
+  if (cus <= 0) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+      (void)hipGetLastError();
+      return E;
+    }
+    if (dev < 64) cu_cache[dev].store(cus, std::memory_order_relaxed);
+  }
+  const int wps = p->waves_per_simd > 0 ? p->waves_per_simd : S64_WPS_DEFAULT;
+  const long long g = (long long)cus * 4 * wps;
+  return g < E ? (int)g : E;
+}
+
 int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* info) {
   if (!p) return fail(SWARM_ENULL, "params is NULL");
   if (p->abi_version != SWARM_ABI_VERSION)
@@ -1433,6 +1748,8 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   if (p->damping_law != 0 && p->damping_law != 1) return fail(SWARM_EINVAL, "damping_law must be 0 or 1");
   if (p->kernel_path != SWARM_PATH_AUTO && p->kernel_path != SWARM_PATH_GENERIC)
     return fail(SWARM_EINVAL, "kernel_path must be SWARM_PATH_AUTO or SWARM_PATH_GENERIC (got %d)", p->kernel_path);
+  if (p->waves_per_simd < 0 || p->waves_per_simd > 8)
+    return fail(SWARM_EINVAL, "waves_per_simd must be in [0, 8] (got %d)", p->waves_per_simd);
 
   KParams k;
   memset(&k, 0, sizeof(k));
@@ -1481,6 +1798,7 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   k.width_w = (float)p->world_size;
   k.dt = (float)p->dt;
   k.vmax = (float)p->max_speed;
+  k.s_vmax = s_threshold(k.vmax);
   k.amax = (float)p->max_accel;
   k.ds_f = (float)p->desired_spacing;
   k.thr_pair = (float)(2.0 * p->collision_radius);
@@ -1538,8 +1856,17 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   kp.pack_bytes = (kp.N == 64 && mode == MODE_STEP && ((uintptr_t)o->terminated | (uintptr_t)o->truncated |
                                                        (uintptr_t)s->active) % 4 == 0) ? 1 : 0;
   if (mode == MODE_STEP && step64_applies(p, kp) && kp.obs_vec4 && kp.pack_bytes) {
-    hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step64()), dim3(kp.E), dim3(64), 0, (hipStream_t)stream,
-                       kp, *s, actions, amask, *o);
+    swarm_state_t st = *s;
+    const int grid = step64_grid(p, kp.E);
+    if (grid >= kp.E) st.work = nullptr;  // one env per workgroup: nothing to dequeue
+    const S64Args args{kp, st, actions, amask, *o};
+    if (st.work)
+      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step64(true)), dim3(grid), dim3(64), 0,
+                         (hipStream_t)stream, args);
+    else
+      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step64(false)),
+                         dim3((kp.E + S64_WG_ENVS - 1) / S64_WG_ENVS), dim3(64 * S64_WG_ENVS), 0, (hipStream_t)stream,
+                         args);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SWARM_OK;
@@ -1625,12 +1952,22 @@ int swarm_query_launch(const swarm_params_t* p, swarm_launch_info_t* info) {
   if (!info) return fail(SWARM_ENULL, "info is NULL");
   const int rc = build_kparams(p, &kp, info);
   if (rc == SWARM_OK && step64_applies(p, kp)) {  // geometry of the step launch (reset/observe stay generic)
-    info->threads_per_block = 64;
-    info->envs_per_block = 1;
+    const int grid = step64_grid(p, kp.E);
+    const int lds_env = (int)(sizeof(float4) * (S64_RING + S64_MMAX) + sizeof(float) * S64_CH * S64_D);
     info->lanes_per_env = 64;
-    info->blocks = kp.E;
-    info->lds_bytes = (int)(sizeof(float4) * (S64_RING + S64_MMAX) + sizeof(float) * S64_CH * S64_D);
-    info->kernel_id = SWARM_KERNEL_STEP64;
+    if (grid < kp.E) {  // persistent grid with env queues (launched when state.work is given)
+      info->threads_per_block = 64;
+      info->envs_per_block = 1;
+      info->blocks = grid;
+      info->lds_bytes = lds_env;
+      info->kernel_id = SWARM_KERNEL_STEP64_PERSISTENT;
+    } else {  // one wave per env, S64_WG_ENVS independent waves per workgroup
+      info->threads_per_block = 64 * S64_WG_ENVS;
+      info->envs_per_block = S64_WG_ENVS;
+      info->blocks = (kp.E + S64_WG_ENVS - 1) / S64_WG_ENVS;
+      info->lds_bytes = S64_WG_ENVS * lds_env;
+      info->kernel_id = SWARM_KERNEL_STEP64;
+    }
   }
   return rc;
 }

@@ -14,12 +14,14 @@ LIB_NAME = "libswarm_mi355x.so"
 LIB_DIR = Path(__file__).resolve().parent / "_lib"
 LIB_PATH = LIB_DIR / LIB_NAME
 
-ABI_VERSION = 2
+ABI_VERSION = 3
+WORK_WORDS = 256  # SWARM_WORK_WORDS: u32 env-queue heads of the persistent swarm_step64
 
 PATH_AUTO = 0
 PATH_GENERIC = 1
 KERNEL_GENERIC = 0
 KERNEL_STEP64 = 1
+KERNEL_STEP64_PERSISTENT = 2
 
 SWARM_OK = 0
 SWARM_EINVAL = -1
@@ -86,13 +88,14 @@ class SwarmParams(ctypes.Structure):
         ("drone_contact_radius", ctypes.c_double),
         ("ground_contact_height", ctypes.c_double),
         ("kernel_path", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("waves_per_simd", ctypes.c_int32),
     ]
 
 
 class SwarmState(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name in
-                ("pos", "vel", "goal", "obstacles", "active", "step_count", "episode", "damping")]
+                ("pos", "vel", "goal", "obstacles", "active", "step_count", "episode", "damping",
+                 "work")]
 
 
 class SwarmOut(ctypes.Structure):

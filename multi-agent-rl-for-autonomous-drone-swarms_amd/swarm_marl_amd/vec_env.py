@@ -38,7 +38,7 @@ class VecSwarm:
                  auto_reset: bool = True, seed: int = 0, env_offset: int = 0,
                  device: str | torch.device | None = None, with_infos: bool = False,
                  with_global_state: bool = False, physics: dict[str, Any] | None = None,
-                 kernel_path: str = "auto"):
+                 kernel_path: str = "auto", persistent: bool = True, waves_per_simd: int = 0):
         if isinstance(config, DroneEnvConfig):
             cfg, raw = config, {}
         else:
@@ -80,6 +80,10 @@ class VecSwarm:
         if kernel_path not in ("auto", "generic"):
             raise ValueError(f"kernel_path must be 'auto' or 'generic', got {kernel_path!r}")
         p.kernel_path = nat.PATH_AUTO if kernel_path == "auto" else nat.PATH_GENERIC
+        if not 0 <= int(waves_per_simd) <= 8:
+            raise ValueError(f"waves_per_simd must be in [0, 8], got {waves_per_simd}")
+        p.waves_per_simd = int(waves_per_simd)
+        self.persistent = bool(persistent)
         for name in ("world_size", "dt", "max_speed", "max_accel", "collision_radius",
                      "goal_radius", "obstacle_radius", "desired_spacing", "reward_progress_scale",
                      "reward_goal", "reward_collision", "reward_formation_scale"):
@@ -105,6 +109,9 @@ class VecSwarm:
         self.step_count = torch.zeros((e,), dtype=torch.int32, **kw)
         self.episode = torch.zeros((e,), dtype=torch.int32, **kw)  # read as uint32 by the kernel
         self.damping = torch.zeros((e, n), dtype=f32, **kw)
+        # env-queue heads of the persistent step kernel (zero, and left zero by every launch)
+        self.work = (torch.zeros((nat.WORK_WORDS,), dtype=torch.int32, **kw)
+                     if self.persistent else None)
         # ---- outputs (persistent buffers)
         self.obs = torch.zeros((e, n, d), dtype=f32, **kw)
         self.reward = torch.zeros((e, n), dtype=f32, **kw)
@@ -124,6 +131,7 @@ class VecSwarm:
         s.obstacles = _ptr(self.obstacles) if self.obstacles.numel() else None
         s.active, s.step_count = _ptr(self.active), _ptr(self.step_count)
         s.episode, s.damping = _ptr(self.episode), _ptr(self.damping)
+        s.work = _ptr(self.work)
         o = nat.SwarmOut()
         o.obs, o.reward = _ptr(self.obs), _ptr(self.reward)
         o.terminated, o.truncated = _ptr(self.terminated), _ptr(self.truncated)
@@ -219,12 +227,16 @@ class VecSwarm:
         return d
 
     def kernel_name(self) -> str:
-        """Kernel the step launches: swarm_step64<16> (headline specialisation) or the generic
-        swarm_kernel<KIND, DYN, KS, MSL, LM> (KIND 0 = step; LM lane mode 0 block / 1
-        multi-team wave / 2 one team per wave)."""
+        """Kernel the step launches: the headline specialisation swarm_step64_once<16, 4> (one
+        wave per env, 4 per workgroup) or its persistent form swarm_step64<16> (E larger than
+        the resident grid, env queues in `work`), else the generic swarm_kernel<KIND, DYN, KS,
+        MSL, LM> (KIND 0 = step; LM lane mode 0 block / 1 multi-team wave / 2 one team per wave)."""
         li = self.launch_info
-        if int(li.kernel_id) == nat.KERNEL_STEP64:
+        kid = int(li.kernel_id)
+        if kid == nat.KERNEL_STEP64_PERSISTENT and self.persistent:
             return "swarm_step64<16>"
+        if kid in (nat.KERNEL_STEP64, nat.KERNEL_STEP64_PERSISTENT):
+            return "swarm_step64_once<16, 4>"
         lanes = int(li.lanes_per_env)
         lm = 0 if lanes > 64 else (2 if lanes == 64 else 1)
         return (f"swarm_kernel<0, {int(self.params.dynamics)}, {int(li.neighbor_slots)}, "

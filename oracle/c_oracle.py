@@ -23,7 +23,7 @@ class Params(ctypes.Structure):  # mirror of swarm_params_t (include/swarm_mi355
             "obstacle_radius", "desired_spacing", "reward_progress_scale", "reward_goal",
             "reward_collision", "reward_formation_scale", "gravity", "gravity_comp", "substep_dt",
             "drone_contact_radius", "ground_contact_height")] + [
-        ("kernel_path", ctypes.c_int32), ("reserved0", ctypes.c_int32)]
+        ("kernel_path", ctypes.c_int32), ("waves_per_simd", ctypes.c_int32)]
 
 
 _LIB = None
@@ -44,7 +44,7 @@ def lib():
 def make_params(cfg: dict, num_envs: int, *, physics=False, auto_reset=False, seed=0,
                 env_offset=0) -> Params:
     p = Params()
-    p.abi_version = 2
+    p.abi_version = 3
     p.num_envs = num_envs
     p.num_drones = int(cfg["num_drones"])
     p.num_obstacles = int(cfg["num_obstacles"])

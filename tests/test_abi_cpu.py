@@ -60,7 +60,7 @@ def _params(nat, lib, **kw):
 
 def test_abi_version_and_defaults(nat, lib):
     from swarm_marl_amd.envs.common import DroneEnvConfig
-    assert lib.swarm_abi_version() == nat.ABI_VERSION == 2
+    assert lib.swarm_abi_version() == nat.ABI_VERSION == 3
     p = _params(nat, lib)
     c = DroneEnvConfig()
     for name in ("max_steps", "num_obstacles", "sensed_obstacles", "neighbor_k"):
@@ -85,7 +85,9 @@ def test_launch_geometry(nat, lib, n):
     assert lib.swarm_query_launch(ctypes.byref(p), ctypes.byref(info)) == 0
     lanes = 1 << (n - 1).bit_length()
     assert info.lanes_per_env == lanes
-    if lanes <= 64:  # wave teams: 64/L envs per 64-thread workgroup
+    if info.kernel_id == nat.KERNEL_STEP64:  # headline specialisation: 4 one-env waves per workgroup
+        assert info.threads_per_block == 256 and info.envs_per_block == 4
+    elif lanes <= 64:  # wave teams: 64/L envs per 64-thread workgroup
         assert info.threads_per_block == 64 and info.envs_per_block == 64 // lanes
     else:  # one env per workgroup of L threads
         assert info.threads_per_block == lanes and info.envs_per_block == 1
@@ -99,7 +101,8 @@ def test_launch_geometry(nat, lib, n):
     ("abi_version", 1, "EINVAL"), ("num_envs", -1, "EINVAL"), ("num_drones", 0, "ELIMIT"),
     ("num_drones", 1025, "ELIMIT"), ("neighbor_k", 17, "ELIMIT"), ("sensed_obstacles", 17, "ELIMIT"),
     ("num_obstacles", -2, "EINVAL"), ("dynamics", 7, "EINVAL"), ("reward_mode", 1, "EINVAL"),
-    ("damping_law", 3, "EINVAL"), ("kernel_path", 2, "EINVAL"),
+    ("damping_law", 3, "EINVAL"), ("kernel_path", 2, "EINVAL"), ("waves_per_simd", 9, "EINVAL"),
+    ("waves_per_simd", -1, "EINVAL"),
 ])
 def test_validation_errors(nat, lib, field, value, code):
     kw = {field: value}

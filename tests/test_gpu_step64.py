@@ -49,7 +49,7 @@ def test_kernel_selection():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     d = torch.device("cuda", 0)
-    assert VecSwarm(4, {"num_drones": 64}, device=d).kernel_name() == "swarm_step64<16>"
+    assert VecSwarm(4, {"num_drones": 64}, device=d).kernel_name() == "swarm_step64_once<16, 4>"
     assert int(VecSwarm(4, {"num_drones": 64}, device=d).launch_info.kernel_id) == nat.KERNEL_STEP64
     for raw in ({"num_drones": 63}, {"num_drones": 64, "neighbor_k": 4},
                 {"num_drones": 64, "sensed_obstacles": 3}, {"num_drones": 64, "num_obstacles": 3},
@@ -68,7 +68,7 @@ def test_step64_matches_generic_autoreset(dev, m, max_steps, masked):
     raw = dict(num_drones=64, num_obstacles=m, max_steps=max_steps)
     e = 2048
     a, b = _pair(dev, raw, e, auto_reset=True, seed=5, env_offset=3)
-    assert a.kernel_name() == "swarm_step64<16>"
+    assert a.kernel_name().startswith("swarm_step64")
     a.reset()
     b.reset()
     _assert_same(a, b, "reset")
@@ -135,7 +135,7 @@ def test_step64_vs_oracle(dev):
     from swarm_marl_amd import VecSwarm
     vec = VecSwarm(e, raw, device=dev, auto_reset=True, seed=21, with_infos=True,
                    with_global_state=True)
-    assert vec.kernel_name() == "swarm_step64<16>"
+    assert vec.kernel_name().startswith("swarm_step64")
     vec.reset()
     torch.cuda.synchronize()
     st = vec_state_numpy(vec)
@@ -157,3 +157,23 @@ def test_step64_vs_oracle(dev):
         for k in ("pos", "vel", "goal", "obst", "active", "step", "episode"):
             assert np.array_equal(got[k], st[k]), f"state {k} t={t}"
         assert np.array_equal(vec.global_state.cpu().numpy(), out["global_state"])
+
+
+@pytest.mark.parametrize("wps,e", [(1, 3000), (2, 2500)])
+def test_step64_persistent_queue_matches_generic(dev, wps, e):
+    """Persistent grid (fewer resident waves than envs): the per-XCD env queues hand out the
+    rest.  Several launches in a row (each must leave the queue heads at zero) with in-kernel
+    resets, bit-identical to the generic kernel; E not a multiple of 8 (ragged head ranges)."""
+    raw = dict(num_drones=64, max_steps=5)
+    a, b = _pair(dev, raw, e, auto_reset=True, seed=13, env_offset=5, waves_per_simd=wps)
+    assert a.kernel_name() == "swarm_step64<16>"
+    assert int(a.launch_info.blocks) < e
+    a.reset()
+    b.reset()
+    g = torch.Generator(device=dev).manual_seed(99)
+    for t in range(8):
+        act = torch.rand((e, 64, 3), device=dev, generator=g) * 2 - 1
+        a.step(act)
+        b.step(act)
+        _assert_same(a, b, f"persistent wps={wps} t={t}")
+        assert int(torch.count_nonzero(a.work)) == 0, "queue heads not reset"

@@ -25,7 +25,7 @@ prof.mkdir(exist_ok=True)
 
 
 def short(name: str) -> str:
-    m = re.search(r"(swarm_kernel<[^>]*>)", name)
+    m = re.search(r"(swarm_(?:kernel|step64_once|step64)<[^>]*>)", name)
     if m:
         return m.group(1)
     return name.split("(")[0][:120]

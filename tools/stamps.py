@@ -16,7 +16,8 @@ NAMES = ["load", "integrate", "pairs+obst", "topk", "reward", "reset", "writebac
 if sys.argv[1] == "build":
     LIB.parent.mkdir(parents=True, exist_ok=True)
     subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-                    "-I", str(ROOT / "include"), "-DSWARM_STAMPS", "-DSWARM_DEV_HOT",
+                    "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
+                    "-I", str(ROOT / "include"), "-DSWARM_STAMPS", "-DSWARM_DEV_HOT", *sys.argv[2:],
                     str(ROOT / "multi-agent-rl-for-autonomous-drone-swarms_amd/csrc/swarm_kernel.hip"),
                     "-o", str(LIB)], check=True)
     sys.exit(0)
@@ -97,3 +98,15 @@ print("longest waves: block, start_us, life_us, phase cycles [load integ pairs t
 for i in o:
     print(f"  {i:5d} {(rt0[i]-rt0.min())/100:7.1f} {life[i]:7.1f} {d[i].tolist()}")
 print("life quantiles us:", np.percentile(life, [50, 90, 99, 99.9, 100]).round(1).tolist())
+
+# ---- timeline: waves alive and waves in each phase, per 2-us bin (realtime clock, 100 MHz)
+mt = buf.reshape(-1, 16)[:, :9].astype(np.int64)
+toff = rt0 - (mt[:, 0] * 100e6 / (clk + 1e-9)).astype(np.int64)  # per-wave realtime offset of memtime 0
+ph_rt = ((mt - mt[:, :1]) / (clk[:, None] / 100e6) + rt0[:, None] - rt0.min()) / 100.0  # us
+bins = np.arange(0, np.ceil(ph_rt.max()) + 2, 2.0)
+print("timeline (us bin: alive | load integ pairs topk reward reset wb obs)")
+for b0 in bins[:-1]:
+    mid = b0 + 1.0
+    alive = int(((ph_rt[:, 0] <= mid) & (ph_rt[:, 8] > mid)).sum())
+    inph = [int(((ph_rt[:, i] <= mid) & (ph_rt[:, i + 1] > mid)).sum()) for i in range(8)]
+    print(f"  {b0:5.0f}: {alive:5d} | " + " ".join(f"{x:5d}" for x in inph))
