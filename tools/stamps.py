@@ -16,7 +16,7 @@ NAMES = ["load", "integrate", "pairs+obst", "topk", "reward", "reset", "writebac
 if sys.argv[1] == "build":
     LIB.parent.mkdir(parents=True, exist_ok=True)
     subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-                    "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
+                    "-fno-slp-vectorize", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
                     "-I", str(ROOT / "include"), "-DSWARM_STAMPS", "-DSWARM_DEV_HOT", *sys.argv[2:],
                     str(ROOT / "multi-agent-rl-for-autonomous-drone-swarms_amd/csrc/swarm_kernel.hip"),
                     "-o", str(LIB)], check=True)
