@@ -114,7 +114,8 @@ typedef struct swarm_params {
   double drone_contact_radius;    /* contact approximation radius of the 0.3x0.3x0.05 box */
   double ground_contact_height;   /* z at or below which the box touches the plane */
   int32_t kernel_path;       /* SWARM_PATH_* (default AUTO) */
-  int32_t waves_per_simd;    /* persistent swarm_step64 grid: resident waves per SIMD (0 = library default) */
+  int32_t waves_per_simd;    /* 0 (default): swarm_step64_once, one wave per env; 1..8: persistent
+                                swarm_step64 grid of that many waves per SIMD (needs state.work) */
 } swarm_params_t;
 
 /* Per-env state, device SoA blocks (all dense, C-contiguous). */
