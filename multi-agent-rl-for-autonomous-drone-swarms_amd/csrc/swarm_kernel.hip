@@ -491,6 +491,26 @@ __device__ __forceinline__ bool exact_pair_collision(const float4* __restrict__ 
   return c;
 }
 
+// step64 observation rows leave through write-through (sc1) buffer stores when SWARM_WT_STORES:
+// the lines are dropped from the XCD's L2 instead of staying dirty for the end-of-kernel
+// write-back (MI355X_MICROARCH.md, store flavours; a kernel boundary pays for the dirty bytes it
+// leaves): -5 % kernel time.  A compiler-visible buffer store (not inline asm) so the hazard and
+// waitcnt passes see it.  `base` must be wave-uniform (it becomes the buffer descriptor).
+#ifndef SWARM_WT_STORES
+#define SWARM_WT_STORES 1
+#endif
+constexpr int BUF_DWORD3 = 0x00020000;  // gfx9 raw buffer descriptor word 3
+__device__ __forceinline__ void store_obs(float* base, uint32_t nbytes, uint32_t byte_off, float4 v) {
+  if constexpr (SWARM_WT_STORES) {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const v4i d = {__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w)};
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)nbytes, BUF_DWORD3);
+    __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)byte_off, 0, 16 /* sc1 */);
+  } else {
+    *reinterpret_cast<float4*>(reinterpret_cast<char*>(base) + byte_off) = v;
+  }
+}
+
 // ------------------------------------------------------------------ the kernel
 // LM (lane mode): 0 = BLOCK (L > 64), 1 = WAVE with 64/L teams, 2 = WAVE with one team (L == 64)
 template <int KIND, int DYN, int KS, int MSL, int LM>
@@ -1072,7 +1092,7 @@ constexpr int S64_RING = 96;
 constexpr int S64_CH = 16;  // obs rows per LDS staging chunk (multiple of 4: 16-B aligned chunks)
 constexpr int S64_HEADS = 8;  // env-queue heads, one per XCD (blockIdx mod 8)
 constexpr int S64_HEAD_STRIDE = SWARM_WORK_WORDS / S64_HEADS;  // one 128-B line per head
-constexpr int S64_WPS_DEFAULT = 8;  // persistent grid: waves per SIMD (8: one wave per env up to E = 8 x 4 x CUs)
+constexpr int S64_WPS_DEFAULT = 0;  // persistent grid only on request (waves_per_simd > 0): slower here
 constexpr int S64_MIN_WAVES = 6;    // register budget of swarm_step64 (<= 80 VGPRs)
 
 // LDS ordering inside one wave: every LDS region of the step64 body belongs to one wave, whose
@@ -1143,7 +1163,10 @@ __device__ __forceinline__ void s64_load(S64ArgPtr A, int env, int t, S64In& c) 
 // One env of the step (all phases) from its prefetched inputs.
 // `prefetch` runs once every input has been consumed (after the integrate phase): it may
 // overwrite `c` with the next env's inputs, whose loads then overlap the rest of this env.
-template <int CH, class Prefetch>
+// LANDED: wait for them (and the queue ticket) after the pair pass, before this env issues any
+// store — vmcnt counts loads and stores in order, so a wait left to the next env's first use would
+// also wait for this env's stores.
+template <int CH, bool LANDED, class Prefetch>
 __device__ __forceinline__ void s64_env(const int env, const int M, const S64In& c, float4* __restrict__ ring,
                                         float4* __restrict__ obst, float* __restrict__ stage, const int lane,
                                         Prefetch&& prefetch) {
@@ -1244,6 +1267,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
 #endif
   else pair_pass_w64<KS, 1, false>(ring, t, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
   obstacle_pass<MSL, true>(obst, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
+  if constexpr (LANDED) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next env's inputs are in
   STAMP_AT(env, 3);
   A = s64_args();
 
@@ -1364,12 +1388,18 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   velE[t3] = vx; velE[t3 + 1] = vy; velE[t3 + 2] = vz;
   {  // terminated, truncated, active: three 64-B rows of bytes built from wave ballots
     const uint64_t m_act = __ballot(new_act);
+    // the three row pointers as uniform SGPR values: a lane-selected kernarg field would become
+    // a per-lane load whose wait also drains every store issued before it
+    uint8_t* p_term = A->O.terminated;
+    uint8_t* p_trunc = A->O.truncated;
+    uint8_t* p_act = A->S.active;
+    asm volatile("" : "+s"(p_term), "+s"(p_trunc), "+s"(p_act));
     const int grp = t >> 4;
     if (grp < 3) {
       const uint64_t m = grp == 0 ? m_term : (grp == 1 ? m_trunc : m_act);
       const uint32_t nib = (uint32_t)(m >> (4 * (t & 15))) & 0xFu;
       const uint32_t word = (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
-      uint8_t* base = grp == 0 ? A->O.terminated : (grp == 1 ? A->O.truncated : A->S.active);
+      uint8_t* base = grp == 0 ? p_term : (grp == 1 ? p_trunc : p_act);
       *reinterpret_cast<uint32_t*>(base + ea + 4 * (t & 15)) = word;
     }
   }
@@ -1454,7 +1484,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     }
     wave_sync();
 #pragma unroll
-    for (int i = t; i < V4; i += 64) dst[ch * V4 + i] = s4[i];
+    for (int i = t; i < V4; i += 64) store_obs(A->O.obs + ea * D, S64_N * D * 4, 16u * (ch * V4 + i), s4[i]);
     wave_sync();
   }
   STAMP_AT(env, 8);
@@ -1520,7 +1550,7 @@ swarm_step64_once(const S64Args args) {
   if (env >= s64_args()->P.E) return;  // whole wave (the last workgroup of a ragged E)
   S64In cur;
   s64_load(s64_args(), env, t, cur);
-  s64_env<CH>(env, s64_args()->P.M, cur, ring[w], obst[w], stage[w], t, []() {});
+  s64_env<CH, false>(env, s64_args()->P.M, cur, ring[w], obst[w], stage[w], t, []() {});
 }
 
 template <int CH>
@@ -1566,9 +1596,13 @@ swarm_step64(const S64Args args) {
   const bool first = env >= 0;
   if (first) s64_load(A, env, t, cur);
   uint32_t ticket = draw();
+  // the first env's inputs and ticket land here, so that no path into the loop header carries a
+  // pending load (the in-loop ones are waited for mid-body, before any store): the header then
+  // needs no vmcnt wait, which would also wait for the previous env's stores
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   while (env >= 0) {
     const int nxt = settle(ticket);
-    s64_env<CH>(env, M, cur, ring, obst, stage, t, [&]() {
+    s64_env<CH, true>(env, M, cur, ring, obst, stage, t, [&]() {
       if (nxt >= 0) {
         s64_load(s64_args(), nxt, t, cur);
         ticket = draw();
@@ -1724,6 +1758,7 @@ int step64_grid(const swarm_params_t* p, int E) {
     if (dev < 64) cu_cache[dev].store(cus, std::memory_order_relaxed);
   }
   const int wps = p->waves_per_simd > 0 ? p->waves_per_simd : S64_WPS_DEFAULT;
+  if (wps <= 0) return E;
   const long long g = (long long)cus * 4 * wps;
   return g < E ? (int)g : E;
 }
