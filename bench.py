@@ -162,7 +162,8 @@ def main():
     wall, timing = wall_eager, "eager launches"
     if not args.no_graph and gather_buf is None:
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # thread_local: the RCCL watchdog thread of a multi-rank run keeps querying its events
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             for k in range(args.ring):
                 vec.step(ring[k])
         graph.replay()  # untimed

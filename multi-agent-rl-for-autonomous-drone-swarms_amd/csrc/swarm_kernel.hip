@@ -133,8 +133,19 @@ __device__ __forceinline__ float sqsum_1d(float x, float y, float z) {
   const float xx = x * x, yy = y * y, zz = z * z;
   return (float)(((double)xx + (double)yy) + (double)zz);
 }
-// np.linalg.norm(A, axis=1): float32 ((x*x)+(y*y))+(z*z).  Also the ranking value s'.
+// np.linalg.norm(A, axis=1): float32 ((x*x)+(y*y))+(z*z).
 __device__ __forceinline__ float sqsum_f(float x, float y, float z) { return ((x * x) + (y * y)) + (z * z); }
+// The 64-lane pair passes' ranking value s': FMA-contracted (3 VALU instead of 5), within two
+// roundings of the exact sum.  Every use is banded (2^-18 >> 2^-21) or re-checked with the exact
+// norms (keys -> finish_keys, running minimum -> exact_pair_collision, formation -> 1e-5 reward
+// contract), so it need not reproduce the reference's bits.
+__device__ __forceinline__ float sqsum_rank(float x, float y, float z) {
+  return __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x));
+}
+// Whole-wave rotate by one lane (DPP wave_ror:1, gfx9): lane i receives lane i-1's value.
+__device__ __forceinline__ float wave_ror1(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x13C, 0xF, 0xF, false));
+}
 
 // np.clip of a float32 in [lo, hi] (lo <= hi): one v_med3_f32
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
@@ -214,7 +225,7 @@ __device__ __forceinline__ float pair_value(float s) {
 }
 template <int KS, int PASS, bool FAST>
 __device__ __forceinline__ uint32_t own_pair(uint32_t (&nk)[KS > 0 ? KS : 1], float s, uint32_t low, bool pr,
-                                             uint32_t keep, float ds, float& smin, float& esum) {
+                                             uint32_t keep, float ds, float& smin, float& esum, float& term) {
   const float v = pair_value<PASS>(s);
   if constexpr (KS > 0) kins<KS>(nk, (__float_as_uint(v) & keep) | low);
   if constexpr (PASS != 0 && (!FAST || KS == 0)) smin = fminf(smin, (FAST || pr) ? v : __builtin_inff());
@@ -224,17 +235,24 @@ __device__ __forceinline__ uint32_t own_pair(uint32_t (&nk)[KS > 0 ? KS : 1], fl
     float e = fabsf(v - ds);
     if constexpr (!FAST) e = pr ? e : 0.f;
     esum += e;
+    term = e;
   }
   return __float_as_uint(v);
 }
 template <int KS, int PASS, bool FAST>
+__device__ __forceinline__ uint32_t own_pair(uint32_t (&nk)[KS > 0 ? KS : 1], float s, uint32_t low, bool pr,
+                                             uint32_t keep, float ds, float& smin, float& esum) {
+  float term;
+  return own_pair<KS, PASS, FAST>(nk, s, low, pr, keep, ds, smin, esum, term);
+}
+template <int KS, int PASS, bool FAST, bool FORM = true>
 __device__ __forceinline__ void mirror_pair(uint32_t (&nk)[KS > 0 ? KS : 1], uint32_t rcv, uint32_t low, bool self,
                                             uint32_t keep_m, float ds, float& smin, float& esum) {
   const float v = __uint_as_float(rcv & 0x7fffffffu);
   const bool pr = FAST || (self && !(rcv >> 31));
   if constexpr (KS > 0) kins<KS>(nk, (rcv & keep_m) | low);
   if constexpr (PASS != 0 && (!FAST || KS == 0)) smin = fminf(smin, pr ? v : __builtin_inff());
-  if constexpr (PASS == 1) {
+  if constexpr (PASS == 1 && FORM) {
     float e = fabsf(v - ds);
     if constexpr (!FAST) e = pr ? e : 0.f;
     esum += e;
@@ -291,48 +309,60 @@ __device__ __forceinline__ void pair_pass_wave(const float4* __restrict__ ring, 
 }
 
 // One team per wave (L = 64): fully unrolled, every LDS / ds_bpermute address is the lane's
-// base plus an immediate offset (ds_bpermute takes the source lane modulo 64).  Rotations are
-// processed in groups of NB (ring reads, distances, ds_bpermutes of a group in flight together);
-// the formation terms of a group are summed in f32, then added to the f64 accumulator.
+// base plus an immediate offset (ds_bpermute takes the source lane modulo 64).  Rotations
+// 31 .. 1 (the ones with a mirror) run in descending groups of NB: ring reads, distances and
+// ds_bpermutes of a group are in flight together.  The mirror keys travel by ds_bpermute; the
+// mirror formation terms do not: the pair term is symmetric (masked by both drones'
+// eligibility, which the sender knows from the ring), so it rides a traveling f32 sum `macc`
+// that rotates one lane per rotation (DPP wave_ror:1, macc = ror(macc) + T_r for r = 31 .. 1,
+// then one more ror): the term of pair (t, t+r) lands on lane t+r.  1 VALU per pair instead of 2
+// on the receiving side.  Own terms are summed in f32 per group, then added in f64.
 #ifndef SWARM_PAIR_BATCH
 #define SWARM_PAIR_BATCH 4
 #endif
-template <int KS, int PASS, bool FAST, int R, int NB, bool MIRROR>
+template <int KS, int PASS, bool FAST, int RT, int NB, bool MIRROR>
 __device__ __forceinline__ void pair_group_w64(const float4* __restrict__ q0, uint32_t t4, float px, float py, float pz,
                                                bool self, uint32_t sflag, uint32_t keep, uint32_t keep_m, float ds,
-                                               uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum) {
+                                               uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum,
+                                               float& macc) {
   float4 q[NB];
-  float sq[NB];
+  float sq[NB], term[NB];
   uint32_t v[NB];
 #pragma unroll
-  for (int i = 0; i < NB; ++i) q[i] = q0[R + i];
+  for (int i = 0; i < NB; ++i) q[i] = q0[RT - i];
 #pragma unroll
-  for (int i = 0; i < NB; ++i) sq[i] = sqsum_f(q[i].x - px, q[i].y - py, q[i].z - pz);
+  for (int i = 0; i < NB; ++i) sq[i] = sqsum_rank(q[i].x - px, q[i].y - py, q[i].z - pz);
   float esum = 0.f;
 #pragma unroll
   for (int i = 0; i < NB; ++i)
-    v[i] = own_pair<KS, PASS, FAST>(nk, sq[i], (uint32_t)(R + i), self & (q[i].w != 0.f), keep, ds, smin, esum);
+    v[i] = own_pair<KS, PASS, FAST>(nk, sq[i], (uint32_t)(RT - i), self & (q[i].w != 0.f), keep, ds, smin, esum,
+                                    term[i]);
   if constexpr (MIRROR) {
     uint32_t rc[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i)
-      rc[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t4 + (uint32_t)(256 - 4 * (R + i))), (int)(v[i] | sflag));
+      rc[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t4 + (uint32_t)(256 - 4 * (RT - i))), (int)(v[i] | sflag));
 #pragma unroll
-    for (int i = 0; i < NB; ++i) mirror_pair<KS, PASS, FAST>(nk, rc[i], (uint32_t)(64 - R - i), self, keep_m, ds, smin, esum);
+    for (int i = 0; i < NB; ++i)
+      mirror_pair<KS, PASS, FAST, false>(nk, rc[i], (uint32_t)(64 - RT + i), self, keep_m, ds, smin, esum);
+    if constexpr (PASS == 1) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) macc = wave_ror1(macc) + term[i];
+    }
   }
   if constexpr (PASS == 1) fsum += (double)esum;
 }
-template <int KS, int PASS, bool FAST, int R, int B>
+template <int KS, int PASS, bool FAST, int RT, int B>
 __device__ __forceinline__ void pair_groups_w64(const float4* __restrict__ q0, uint32_t t4, float px, float py, float pz,
                                                 bool self, uint32_t sflag, uint32_t keep, uint32_t keep_m, float ds,
-                                                uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum) {
-  // rotations R .. 31 carry a mirror; rotation 32 pairs t with t+32 from both sides (own only)
-  if constexpr (R <= 31) {
-    constexpr int NB = (31 - R + 1) < B ? (31 - R + 1) : B;
-    pair_group_w64<KS, PASS, FAST, R, NB, true>(q0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum);
-    pair_groups_w64<KS, PASS, FAST, R + NB, B>(q0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum);
-  } else {
-    pair_group_w64<KS, PASS, FAST, 32, 1, false>(q0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum);
+                                                uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum,
+                                                float& macc) {
+  if constexpr (RT >= 1) {
+    constexpr int NB = RT < B ? RT : B;
+    pair_group_w64<KS, PASS, FAST, RT, NB, true>(q0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum,
+                                                 macc);
+    pair_groups_w64<KS, PASS, FAST, RT - NB, B>(q0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum,
+                                                macc);
   }
 }
 template <int KS, int PASS, bool FAST>
@@ -342,8 +372,13 @@ __device__ __forceinline__ void pair_pass_w64(const float4* __restrict__ ring, i
   const uint32_t sflag = (FAST || self) ? 0u : 0x80000000u;
   const uint32_t keep_m = keep & 0x7fffffffu;
   const uint32_t t4 = (uint32_t)t << 2;
-  pair_groups_w64<KS, PASS, FAST, 1, SWARM_PAIR_BATCH>(ring + t, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin,
-                                                       fsum);
+  float macc = 0.f;
+  pair_groups_w64<KS, PASS, FAST, 31, SWARM_PAIR_BATCH>(ring + t, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk,
+                                                        smin, fsum, macc);
+  if constexpr (PASS == 1) fsum += (double)wave_ror1(macc);
+  // rotation 32 pairs t with t+32 from both sides: own evaluation only
+  pair_group_w64<KS, PASS, FAST, 32, 1, false>(ring + t, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum,
+                                               macc);
 }
 
 template <int KS, int PASS>
@@ -394,14 +429,14 @@ __device__ __forceinline__ bool finish_keys(const uint32_t (&k)[S], const float4
   bool near = false;
 #pragma unroll
   for (int s = 0; s + 1 < S; ++s)
-    near = near || (k[s + 1] != KEY_EMPTY &&
-                    __uint_as_float(k[s + 1] & keep) <= __uint_as_float((k[s] & keep) | imask) * FAST_HI);
+    near = near | ((k[s + 1] != KEY_EMPTY) &
+                   (__uint_as_float(k[s + 1] & keep) <= __uint_as_float((k[s] & keep) | imask) * FAST_HI));
   const int need = near ? S : K;
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const uint32_t key = k[s];
     const int j = ((int)(key & imask) + ibase) & imod;
-    const bool valid = (key != KEY_EMPTY) && (j < count) && (s < need);
+    const bool valid = (key != KEY_EMPTY) & (j < count) & (s < need);
     float d = __builtin_inff();
     if (valid) {
       const float4 q = pts[j];
