@@ -1124,7 +1124,14 @@ constexpr int S64_MS = 4;
 constexpr int S64_D = 9 + 4 * S64_K + 4 * S64_MS;  // 37
 constexpr int S64_MMAX = 16;
 constexpr int S64_RING = 96;
-constexpr int S64_CH = 16;  // obs rows per LDS staging chunk (multiple of 4: 16-B aligned chunks)
+// obs rows per LDS staging chunk (multiple of 4: 16-B aligned chunks).  The staging buffer
+// aliases the wave's ring and obstacles (dead once the rows are built in registers), so 32-row
+// chunks (4.6 KB per wave, 148 KB for 32 waves per CU) fit: half the chunk passes and LDS row
+// writes of 16-row chunks.
+#ifndef SWARM_S64_CH
+#define SWARM_S64_CH 32
+#endif
+constexpr int S64_CH = SWARM_S64_CH;
 constexpr int S64_HEADS = 8;  // env-queue heads, one per XCD (blockIdx mod 8)
 constexpr int S64_HEAD_STRIDE = SWARM_WORK_WORDS / S64_HEADS;  // one 128-B line per head
 constexpr int S64_WPS_DEFAULT = 0;  // persistent grid only on request (waves_per_simd > 0): slower here
@@ -1141,6 +1148,16 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+// A wave's LDS: ring + obstacles during the step, the obs staging chunk afterwards.
+template <int CH>
+union S64Lds {
+  struct {
+    float4 ring[S64_RING];
+    float4 obst[S64_MMAX];
+  } w;
+  float4 stage[CH * S64_D / 4];
+};
 
 // One env's inputs, loaded one env ahead of its compute (software pipeline): raw loaded values
 // only — any arithmetic on them here would make the wave wait for the loads right away.
@@ -1493,6 +1510,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   }
   if (SWARM_ABLATE & ABL_STAGE_ONLY) {  // diagnostic: the LDS staging without the obs stores
     float acc = 0.f;
+    wave_sync();
     float* srow0 = stage + (t % CH) * D;
 #pragma unroll
     for (int ch = 0; ch < S64_N / CH; ++ch) {
@@ -1509,6 +1527,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     if (acc == 12345.f) dst[t] = make_float4(acc, acc, acc, acc);
     return;
   }
+  wave_sync();  // the stage aliases ring / obstacles: every row-build read is issued before it
   const float4* s4 = reinterpret_cast<const float4*>(stage);
   float* srow = stage + (t % CH) * D;
 #pragma unroll
@@ -1574,9 +1593,7 @@ template <int CH, int G>
 __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(8)))
 swarm_step64_once(const S64Args args) {
   (void)args;  // read through s64_args()
-  __shared__ float4 ring[G][S64_RING];
-  __shared__ float4 obst[G][S64_MMAX];
-  __shared__ __attribute__((aligned(16))) float stage[G][CH * S64_D];
+  __shared__ S64Lds<CH> lds[G];
   s64_set_priority();
   if constexpr (SWARM_PRIO_MODE >= 2) __builtin_amdgcn_s_setprio(3);  // inputs and integrate first
   const int t = threadIdx.x & 63;
@@ -1585,16 +1602,18 @@ swarm_step64_once(const S64Args args) {
   if (env >= s64_args()->P.E) return;  // whole wave (the last workgroup of a ragged E)
   S64In cur;
   s64_load(s64_args(), env, t, cur);
-  s64_env<CH, false>(env, s64_args()->P.M, cur, ring[w], obst[w], stage[w], t, []() {});
+  s64_env<CH, false>(env, s64_args()->P.M, cur, lds[w].w.ring, lds[w].w.obst,
+                     reinterpret_cast<float*>(lds[w].stage), t, []() {});
 }
 
 template <int CH>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(S64_MIN_WAVES)))
 swarm_step64(const S64Args args) {
   (void)args;  // read through s64_args()
-  __shared__ float4 ring[S64_RING];
-  __shared__ float4 obst[S64_MMAX];
-  __shared__ __attribute__((aligned(16))) float stage[CH * S64_D];
+  __shared__ S64Lds<CH> lds;
+  float4* const ring = lds.w.ring;
+  float4* const obst = lds.w.obst;
+  float* const stage = reinterpret_cast<float*>(lds.stage);
   const int t = threadIdx.x;
   uint32_t* head = nullptr;
   int env, base = 0;
@@ -2023,7 +2042,7 @@ int swarm_query_launch(const swarm_params_t* p, swarm_launch_info_t* info) {
   const int rc = build_kparams(p, &kp, info);
   if (rc == SWARM_OK && step64_applies(p, kp)) {  // geometry of the step launch (reset/observe stay generic)
     const int grid = step64_grid(p, kp.E);
-    const int lds_env = (int)(sizeof(float4) * (S64_RING + S64_MMAX) + sizeof(float) * S64_CH * S64_D);
+    const int lds_env = (int)sizeof(S64Lds<S64_CH>);
     info->lanes_per_env = 64;
     if (grid < kp.E) {  // persistent grid with env queues (launched when state.work is given)
       info->threads_per_block = 64;

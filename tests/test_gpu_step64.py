@@ -49,7 +49,7 @@ def test_kernel_selection():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     d = torch.device("cuda", 0)
-    assert VecSwarm(4, {"num_drones": 64}, device=d).kernel_name() == "swarm_step64_once<16, 4>"
+    assert VecSwarm(4, {"num_drones": 64}, device=d).kernel_name() == "swarm_step64_once<32, 4>"
     assert int(VecSwarm(4, {"num_drones": 64}, device=d).launch_info.kernel_id) == nat.KERNEL_STEP64
     for raw in ({"num_drones": 63}, {"num_drones": 64, "neighbor_k": 4},
                 {"num_drones": 64, "sensed_obstacles": 3}, {"num_drones": 64, "num_obstacles": 3},
@@ -166,7 +166,7 @@ def test_step64_persistent_queue_matches_generic(dev, wps, e):
     resets, bit-identical to the generic kernel; E not a multiple of 8 (ragged head ranges)."""
     raw = dict(num_drones=64, max_steps=5)
     a, b = _pair(dev, raw, e, auto_reset=True, seed=13, env_offset=5, waves_per_simd=wps)
-    assert a.kernel_name() == "swarm_step64<16>"
+    assert a.kernel_name() == "swarm_step64<32>"
     assert int(a.launch_info.blocks) < e
     a.reset()
     b.reset()
