@@ -1537,8 +1537,16 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       for (int i = 0; i < D; ++i) srow[i] = row[i];
     }
     wave_sync();
+    // all of the chunk's LDS reads in flight before the first store (a rolled `i += 64` loop
+    // pays one LDS round trip per 1 KB)
+    constexpr int NF = V4 / 64, NR = V4 % 64;
+    float4 v[NF + 1];
 #pragma unroll
-    for (int i = t; i < V4; i += 64) store_obs(A->O.obs + ea * D, S64_N * D * 4, 16u * (ch * V4 + i), s4[i]);
+    for (int k = 0; k < NF; ++k) v[k] = s4[t + 64 * k];
+    if (NR && t < NR) v[NF] = s4[t + 64 * NF];
+#pragma unroll
+    for (int k = 0; k < NF; ++k) store_obs(A->O.obs + ea * D, S64_N * D * 4, 16u * (ch * V4 + t + 64 * k), v[k]);
+    if (NR && t < NR) store_obs(A->O.obs + ea * D, S64_N * D * 4, 16u * (ch * V4 + t + 64 * NF), v[NF]);
     wave_sync();
   }
   STAMP_AT(env, 8);

@@ -40,7 +40,7 @@ acts = [torch.rand((e, n, 3), device="cuda:0", generator=g) * 2 - 1 for _ in ran
 for k in range(20):
     vec.step(acts[k % 4])
 torch.cuda.synchronize()
-blocks = vec.launch_info.blocks
+blocks = e  # one stamp record per env
 buf = np.zeros(min(blocks, 1 << 16) * 16, np.uint64)
 lib.swarm_debug_stamps(buf.ctypes.data, buf.size)
 st = buf.reshape(-1, 16)[:, :9].astype(np.int64)
