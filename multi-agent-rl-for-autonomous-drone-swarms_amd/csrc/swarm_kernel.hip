@@ -1538,7 +1538,13 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     }
     wave_sync();
     // all of the chunk's LDS reads in flight before the first store (a rolled `i += 64` loop
-    // pays one LDS round trip per 1 KB)
+    // pays one LDS round trip per 1 KB).  The persistent loop (LANDED) has no registers to spare
+    // for the 5 float4 and keeps the loop.
+    if constexpr (LANDED) {
+      for (int i = t; i < V4; i += 64) store_obs(A->O.obs + ea * D, S64_N * D * 4, 16u * (ch * V4 + i), s4[i]);
+      wave_sync();
+      continue;
+    }
     constexpr int NF = V4 / 64, NR = V4 % 64;
     float4 v[NF + 1];
 #pragma unroll
