@@ -1,32 +1,40 @@
 #!/usr/bin/env python3
 """Headline benchmark: agent-steps/s of the fused swarm step at N=64 drones x E=8192 envs/GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config headline|n16|n256]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 One step = one launch of the fused kernel over the local env shard (integrate, distances,
 collision, formation, rewards, terminations, in-kernel auto-reset, kNN obs) with inputs resident
 in HBM.  Envs are sharded across ranks with no collective on the step path (weak scaling:
-8192 envs per GPU).  The K timed steps run twice: eagerly with HIP events around every launch
-(per-launch kernel time for the roofline) and as hipGraph replays of the action-ring segment
-(`value`: the whole-job rate without per-step host launch cost; --no-graph times the eager
-loop instead).  Rank 0 prints ONE JSON line.  `roofline.achieved` = algorithmic HBM bytes
-per launch / mean kernel duration from HIP events on the launch stream;
-`cpu_baseline` = the C oracle (oracle/swarm_oracle.c, a port of the reference step) timed on the
-host cores for a bounded sample of the same workload.
+`--envs` envs per GPU, rank r owns the global envs [r*E, (r+1)*E)).
+
+Timing (the driver's contract): W untimed warm-up steps, then exactly K timed steps bracketed by
+a barrier + device synchronize on both sides, the max over ranks.  The K steps are replayed from
+a hipGraph holding one launch per action tensor of the ring (`value`, `ms_per_step`: the whole-job
+rate without per-step host launch cost); HIP events recorded on the launch stream around that
+timed region give the average launch duration (`roofline.kernel_ms_mean`, the roofline's time
+base; compare `rocprofv3 --kernel-trace --stats` in profiles/).  A second, eager pass with one
+event pair per launch is reported as `ms_per_step_eager` / `kernel_ms_eager_events`.
+`--ctde` also emits the CTDE global_state and all-gathers it every `--gather-every` steps over
+RCCL (config 5; eager timing).
+
+`cpu_baseline` = the C port of the reference step (oracle/swarm_oracle.c) on the host cores for
+a bounded sample of the same workload; `cpu_baseline_variants` = the per-agent loop restatement
+(like the reference `DroneSwarmEnv.step`) and the vectorised NumPy restatement, one process per
+core.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 from pathlib import Path
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "multi-agent-rl-for-autonomous-drone-swarms_amd"))
@@ -34,19 +42,35 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "agent-steps/sec at N=64 × E=8192 envs, 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+VALU_PEAK_LANE_OPS = 78.6e12  # f32 VALU lane-ops/s (157.3 TFLOP/s counting FMA as 2); SURVEY §8d
+
+# BASELINE.json configs, per GPU: [2] is the headline (the metric's config), [1] and [4] have
+# their own bench lines (profiles/r02_config_lines.jsonl).
+PRESETS = {
+    "headline": dict(drones=64, envs=8192, ctde=False,
+                     label="config 3: N=64 x E=8192 on 1 MI355X (headline); config 4 per GPU"),
+    "n16": dict(drones=16, envs=1024, ctde=False,
+                label="config 2: N=16 x E=1024 on 1 MI355X (launch-latency-bound)"),
+    "n256": dict(drones=256, envs=1024, ctde=True,
+                 label="config 5 per-GPU slab: N=256 x E=1024 with CTDE global_state"),
+}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--drones", type=int, default=64)
-    ap.add_argument("--envs", type=int, default=8192, help="envs per GPU")
+    ap.add_argument("--config", choices=sorted(PRESETS), default="headline")
+    ap.add_argument("--drones", type=int, default=None)
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU")
     ap.add_argument("--no-term", action="store_true",
                     help="no-termination variant (collision/goal radii 0)")
     ap.add_argument("--ring", type=int, default=8, help="distinct pre-generated action tensors")
-    ap.add_argument("--cpu-seconds", type=float, default=3.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="timed seconds of the C-port CPU baseline")
+    ap.add_argument("--cpu-variant-seconds", type=float, default=3.0,
+                    help="timed seconds of each Python restatement variant (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--waves-per-simd", type=int, default=0,
                     help="persistent step kernel: resident waves per SIMD (0 = library default)")
@@ -54,58 +78,150 @@ def parse():
                     help="one workgroup per env instead of the persistent env queue")
     ap.add_argument("--no-graph", action="store_true",
                     help="time the whole-job rate with eager launches instead of hipGraph replay")
-    ap.add_argument("--ctde", action="store_true",
-                    help="also emit global_state and all-gather it every step (config 5)")
-    return ap.parse_args()
+    ap.add_argument("--ctde", action="store_true", default=None,
+                    help="also emit global_state and all-gather it (config 5)")
+    ap.add_argument("--gather-every", type=int, default=8,
+                    help="CTDE all-gather period in steps (SURVEY.md §5: per batch, not per step)")
+    a = ap.parse_args(argv)
+    pre = PRESETS[a.config]
+    a.drones = pre["drones"] if a.drones is None else a.drones
+    a.envs = pre["envs"] if a.envs is None else a.envs
+    a.ctde = pre["ctde"] if a.ctde is None else a.ctde
+    a.label = pre["label"]
+    if a.gather_every < 1:
+        ap.error("--gather-every must be >= 1")
+    return a
 
 
-def cpu_baseline(cfg_raw: dict, n: int, seconds: float) -> dict:
-    """C oracle on the host cores: bounded sample of the same workload (auto-reset on)."""
+# ----------------------------------------------------------------------------- rank logic
+def shard_plan(world: int, rank: int, envs_per_gpu: int) -> tuple[int, int]:
+    """(env_offset, count) of `rank`: weak scaling, each rank owns envs_per_gpu global envs."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} / world {world}")
+    return rank * envs_per_gpu, envs_per_gpu
+
+
+def max_over_ranks(values, world: int, device=None) -> list[float]:
+    """Element-wise MAX of per-rank floats (a tiny all_reduce outside the timed region)."""
+    import torch
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.cpu()]
+
+
+def timed_region(body, world: int, sync) -> float:
+    """Barrier + sync, run `body`, sync + barrier; wall seconds of this rank."""
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    body()
+    sync()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def gather_schedule(steps: int, every: int) -> list[int]:
+    """Timed-step indices after which the CTDE all-gather runs (every `every` steps + the last)."""
+    ks = [k for k in range(steps) if (k + 1) % every == 0]
+    if steps and (not ks or ks[-1] != steps - 1):
+        ks.append(steps - 1)
+    return ks
+
+
+# ----------------------------------------------------------------------------- CPU baselines
+def _cpu_cores() -> tuple[int, str]:
+    """Host cores this process may use: the affinity set, capped by OMP_NUM_THREADS when the
+    harness sets it to the box's CPU share (os.cpu_count() shows the whole machine there)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and 0 < int(omp) < aff:
+        return int(omp), f"{omp} threads = OMP_NUM_THREADS (this host's CPU share; {aff} in the affinity set)"
+    return aff, f"{aff} threads = every core of the affinity set"
+
+
+def cpu_baseline_port(n: int, e: int, seconds: float, raw: dict) -> dict:
+    """C port of the reference step (oracle/swarm_oracle.c, OpenMP) on the benched workload:
+    same N and E, auto-reset on, persistent buffers, a bounded number of steps."""
     from oracle import c_oracle as co
     from oracle import swarm_oracle as so
 
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:  # pragma: no cover
-        cores = os.cpu_count() or 1
-    threads = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
-    cfg = so.make_cfg(**cfg_raw)
-    e = 64 * threads
-    st = so.empty_state(cfg, e)
-    st, _ = co.run(cfg, st, "reset", seed=0, nthreads=threads)
+    cores, why = _cpu_cores()
+    cfg = so.make_cfg(**raw)
+    run = co.Runner(cfg, e, seed=0, nthreads=cores)
     rng = np.random.default_rng(1000)
     ring = [rng.uniform(-1, 1, (e, n, 3)).astype(np.float32) for _ in range(4)]
-    co.run(cfg, st, "step", ring[0], auto_reset=True, nthreads=threads)  # warm
+    run.step(ring[0])  # warm
     steps, t0 = 0, time.perf_counter()
     while True:
-        st, _ = co.run(cfg, st, "step", ring[steps % 4], auto_reset=True, seed=0,
-                       nthreads=threads)
+        run.step(ring[steps % 4])
         steps += 1
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": e * n * steps / el, "unit": "agent-steps/s", "cores": threads,
-            "kind": "port",
-            "sample": f"C oracle (port of DroneSwarmEnv.step, oracle/swarm_oracle.c), OpenMP "
-                      f"{threads} threads, N={n} x E={e} envs, {steps} steps in {el:.2f} s, "
-                      f"auto-reset on; includes ctypes call overhead per step"}
+    return {"value": e * n * steps / el, "unit": "agent-steps/s", "cores": cores, "kind": "port",
+            "sample": f"C port of DroneSwarmEnv.step (oracle/swarm_oracle.c), OpenMP {why}; "
+                      f"N={n} x E={e} envs (the benched workload), {steps} steps in {el:.2f} s, "
+                      f"auto-reset on, bit-exact with the reference fixtures"}
 
 
-def pmc_traffic(workload_key: str):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if one matches."""
+def cpu_python_variants(n: int, e: int, seconds: float, procs: int | None = None) -> list[dict]:
+    """BASELINE.md §5 (a) per-agent loop restatement and (b) vectorised NumPy restatement, one
+    single-threaded process per core with the envs split across them."""
+    if procs is None:
+        procs, _ = _cpu_cores()
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1",
+               PYTHONPATH=os.pathsep.join([str(ROOT), os.environ.get("PYTHONPATH", "")]))
+    out = []
+    for kind, desc in (("loop", "per-agent loop restatement (oracle/swarm_loop.py, the reference "
+                                "DroneSwarmEnv.step's structure)"),
+                       ("numpy", "vectorised NumPy restatement (oracle/swarm_oracle.py)")):
+        per = max(1, e // procs) if kind == "numpy" else max(1, min(4, e // procs))
+        ps = [subprocess.Popen([sys.executable, "-m", "oracle.cpu_bench", "--kind", kind,
+                                "--drones", str(n), "--envs", str(per), "--seconds", str(seconds),
+                                "--seed", str(k)], stdout=subprocess.PIPE, cwd=str(ROOT), env=env)
+              for k in range(procs)]
+        res = []
+        for p in ps:
+            so_, _ = p.communicate(timeout=seconds * 20 + 120)
+            if p.returncode != 0:
+                raise RuntimeError(f"cpu_bench {kind} failed ({p.returncode})")
+            res.append(json.loads(so_.decode().strip().splitlines()[-1]))
+        total = sum(r["agent_steps"] for r in res)
+        el = max(r["seconds"] for r in res)
+        out.append({"value": total / el, "unit": "agent-steps/s", "cores": procs, "kind": "port",
+                    "sample": f"{desc}: {procs} single-threaded processes x {per} envs of N={n}, "
+                              f"{total} agent-steps in {el:.2f} s, auto-reset on"})
+    return out
+
+
+# ----------------------------------------------------------------------------- profile data
+def profile_record(workload_key: str):
+    """Counter data for this workload from the committed rocprofv3 PMC summary (not measured in
+    this run): HBM bytes per launch and VALU instructions per launch."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
         return None
     try:
-        d = json.loads(f.read_text())
+        return json.loads(f.read_text()).get(workload_key)
     except Exception:
         return None
-    rec = d.get(workload_key)
-    return None if rec is None else rec.get("hbm_bytes_per_launch")
 
 
-def main():
-    args = parse()
+# ----------------------------------------------------------------------------- main
+def main(argv=None):
+    import torch
+    import torch.distributed as dist
+
+    args = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -117,50 +233,37 @@ def main():
 
     from swarm_marl_amd import VecSwarm
 
-    n, e = args.drones, args.envs
+    n = args.drones
+    offset, e = shard_plan(world, rank, args.envs)
     raw = {"num_drones": n}
     if args.no_term:
         raw.update(collision_radius=0.0, obstacle_radius=0.0, goal_radius=0.0)
-    vec = VecSwarm(e, raw, device=dev, auto_reset=True, seed=0, env_offset=rank * e,
+    vec = VecSwarm(e, raw, device=dev, auto_reset=True, seed=0, env_offset=offset,
                    with_global_state=args.ctde, persistent=not args.no_persistent,
                    waves_per_simd=args.waves_per_simd)
     vec.reset()
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     ring = [torch.rand((e, n, 3), device=dev, generator=gen) * 2 - 1 for _ in range(args.ring)]
     gather_buf = None
+    gathers = set()
     if args.ctde and world > 1:
         gather_buf = torch.empty((world * e, 6 * n + 3), device=dev)
+        gathers = set(gather_schedule(args.steps, args.gather_every))
 
-    def one(k):
+    def step(k):
         vec.step(ring[k % args.ring])
-        if gather_buf is not None:
+        if gather_buf is not None and k in gathers:
             dist.all_gather_into_tensor(gather_buf, vec.global_state)
 
     for k in range(args.warmup):
-        one(k)
+        step(k)
     stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record(stream)
-        vec.step(ring[k % args.ring])
-        ev[k][1].record(stream)
-        if gather_buf is not None:
-            dist.all_gather_into_tensor(gather_buf, vec.global_state)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    wall_eager = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
 
-    # Whole-job rate: the same K steps replayed from a hipGraph that holds one step launch per
-    # action tensor of the ring (host launch cost off the step path, as in a captured rollout).
-    wall, timing = wall_eager, "eager launches"
-    if not args.no_graph and gather_buf is None:
+    # ---- timed region: hipGraph replay of ring segments (or eager with --no-graph / CTDE)
+    t_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    use_graph = not args.no_graph and gather_buf is None
+    if use_graph:
         graph = torch.cuda.CUDAGraph()
         # thread_local: the RCCL watchdog thread of a multi-rank run keeps querying its events
         with torch.cuda.graph(graph, capture_error_mode="thread_local"):
@@ -168,55 +271,90 @@ def main():
                 vec.step(ring[k])
         graph.replay()  # untimed
         reps, rem = divmod(args.steps, args.ring)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            graph.replay()
-        for k in range(rem):
-            vec.step(ring[k])
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        wall = time.perf_counter() - t0
+
+        def body():
+            t_ev[0].record(stream)
+            for _ in range(reps):
+                graph.replay()
+            for k in range(rem):
+                vec.step(ring[k])
+            t_ev[1].record(stream)
         timing = f"hipGraph replay of {args.ring}-step segments"
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall, kern_ms_max = float(t[0]), float(t[1])
+    else:
+        def body():
+            t_ev[0].record(stream)
+            for k in range(args.steps):
+                step(k)
+            t_ev[1].record(stream)
+        timing = "eager launches" + (f", CTDE all-gather every {args.gather_every} steps"
+                                     if gather_buf is not None else "")
+    wall = timed_region(body, world, sync)
+    kern_ms = t_ev[0].elapsed_time(t_ev[1]) / args.steps
+
+    # ---- diagnostic pass: eager launches, one event pair around every launch
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+
+    def body_eager():
+        for k in range(args.steps):
+            ev[k][0].record(stream)
+            vec.step(ring[k % args.ring])
+            ev[k][1].record(stream)
+    wall_eager = timed_region(body_eager, world, sync)
+    kern_eager = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    wall_max, kern_max, eager_max, kern_eager_max = max_over_ranks(
+        [wall, kern_ms, wall_eager, kern_eager], world, dev)
     done_frac = float((vec.env_done != 0).float().mean())
 
     if rank == 0:
         total = world * e * n * args.steps
-        value = total / wall
+        value = total / wall_max
         bytes_launch = vec.algorithmic_bytes_per_step()
-        achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-        wl = f"kinematic+swarm N={n} E={e}{' noterm' if args.no_term else ''}"
+        achieved = bytes_launch / (kern_max * 1e-3) / 1e9
+        wl = f"kinematic+swarm N={n} E={e}{' noterm' if args.no_term else ''}" + \
+             (" +global_state" if args.ctde else "")
+        prof = profile_record(wl) or {}
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": prof.get("hbm_bytes_per_launch"),
+                "traffic_source": (f"rocprofv3 PMC (2 x FETCH_SIZE + WRITE_SIZE) of this workload, "
+                                   f"profiles/pmc_traffic.json round {prof.get('round')}; not "
+                                   f"measured in this run") if prof else None,
+                "algorithmic_bytes_per_launch": bytes_launch,
+                "kernel_ms_mean": kern_max,
+                "kernel_ms_timing": "HIP events on the launch stream around the timed region "
+                                    "(graph replays), / K; max over ranks",
+                "kernel_ms_eager_events": kern_eager_max,
+                "kernel": vec.kernel_name(),
+                "grid": int(vec.launch_info.blocks)}
+        if prof.get("valu_insts_per_launch"):
+            lane_ops = prof["valu_insts_per_launch"] * 64.0
+            roof["valu"] = {"achieved_lane_ops_per_s": lane_ops / (kern_max * 1e-3),
+                            "peak": VALU_PEAK_LANE_OPS,
+                            "frac": lane_ops / (kern_max * 1e-3) / VALU_PEAK_LANE_OPS,
+                            "source": "SQ_INSTS_VALU x 64 lanes from profiles/pmc_traffic.json"}
         rec = {
             "metric": METRIC, "value": value, "unit": "agent-steps/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
-            "ms_per_step_eager": wall_eager / args.steps * 1e3, "step_timing": timing,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall_max / args.steps * 1e3,
+            "ms_per_step_eager": eager_max / args.steps * 1e3, "step_timing": timing,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (device-RNG episodes, uniform(-1,1) actions)",
             "config": {"workload": f"N={n} drones x E={e} envs per GPU, kinematic dynamics + "
                                    f"swarm reward, in-kernel auto-reset"
-                                   f"{', no-termination radii' if args.no_term else ''}",
+                                   f"{', no-termination radii' if args.no_term else ''}"
+                                   f"{', CTDE global_state emitted' if args.ctde else ''}",
+                       "baseline_config": args.label,
                        "num_drones": n, "envs_per_gpu": e, "global_envs": world * e,
                        "obs_dim": vec.obs_dim, "parallelism": f"env-sharded x{world}",
-                       "ctde_allgather": bool(args.ctde and world > 1)},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic(wl),
-                         "algorithmic_bytes_per_launch": bytes_launch,
-                         "kernel_ms_mean": kern_ms, "kernel_ms_mean_max_rank": kern_ms_max,
-                         "kernel": vec.kernel_name(),
-                         "grid": int(vec.launch_info.blocks) if vec.persistent else e,
-                         "timing": "HIP events on the launch stream around each step"},
+                       "ctde_allgather": bool(gather_buf is not None),
+                       "ctde_gather_every": args.gather_every if gather_buf is not None else None},
+            "roofline": roof,
             "env_done_fraction_last_step": done_frac,
         }
         if not args.no_cpu_baseline and world == 1:
-            rec["cpu_baseline"] = cpu_baseline(raw, n, args.cpu_seconds)
+            rec["cpu_baseline"] = cpu_baseline_port(n, e, args.cpu_seconds, raw)
+            if args.cpu_variant_seconds > 0 and not args.no_term:
+                rec["cpu_baseline_variants"] = cpu_python_variants(n, e, args.cpu_variant_seconds)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

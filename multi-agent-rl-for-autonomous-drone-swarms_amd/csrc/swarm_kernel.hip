@@ -70,7 +70,7 @@ __device__ unsigned long long g_stamps[1 << 20];
     unsigned long long ts_;                                                              \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");           \
     __builtin_amdgcn_sched_barrier(0);                                                   \
-    if (threadIdx.x == 0 && (rec) < (1 << 16)) g_stamps[(rec) * 16 + (i)] = ts_;           \
+    if ((threadIdx.x & 63) == 0 && (rec) < (1 << 16)) g_stamps[(rec) * 16 + (i)] = ts_;           \
   } while (0)
 #else
 #define STAMP_AT(rec, i) do {} while (0)
@@ -1234,7 +1234,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   S64ArgPtr A = s64_args();  // re-fetched at every phase boundary
   STAMP_AT(env, 0);
 #ifdef SWARM_STAMPS
-  if (threadIdx.x == 0 && env < (1 << 16)) g_stamps[env * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0 && env < (1 << 16)) g_stamps[env * 16 + 11] = __builtin_amdgcn_s_memrealtime();
 #endif
 
   // ---- inputs (prefetched): env-uniform scalars, per-lane rows, obstacles to LDS
@@ -1557,7 +1557,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   }
   STAMP_AT(env, 8);
 #ifdef SWARM_STAMPS
-  if (threadIdx.x == 0 && env < (1 << 16)) {
+  if ((threadIdx.x & 63) == 0 && env < (1 << 16)) {
     g_stamps[env * 16 + 9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
     g_stamps[env * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
     g_stamps[env * 16 + 12] = __builtin_amdgcn_s_memrealtime();

@@ -119,3 +119,39 @@ def philox4x32_10(ctr, key):
 
 def max_threads() -> int:
     return int(lib().oracle_max_threads())
+
+
+class Runner:
+    """Persistent-buffer stepping of the C oracle (no per-call copies or allocations): the
+    bench's CPU-baseline loop.  State arrays are updated in place by every call."""
+
+    def __init__(self, cfg: dict, num_envs: int, *, seed=0, env_offset=0, nthreads=0):
+        self.cfg, self.e, self.seed, self.nthreads = cfg, int(num_envs), int(seed), int(nthreads)
+        n, m = int(cfg["num_drones"]), int(cfg["num_obstacles"])
+        d = 9 + 4 * max(int(cfg["neighbor_k"]), 0) + 4 * max(int(cfg["sensed_obstacles"]), 0)
+        e = self.e
+        self.st = dict(pos=np.zeros((e, n, 3), np.float32), vel=np.zeros((e, n, 3), np.float32),
+                       goal=np.zeros((e, 3), np.float32), obst=np.zeros((e, m, 3), np.float32),
+                       active=np.ones((e, n), np.uint8), step=np.zeros(e, np.int32),
+                       episode=np.zeros(e, np.uint32), damping=np.zeros((e, n), np.float32))
+        self.out = dict(obs=np.zeros((e, n, d), np.float32), reward=np.zeros((e, n), np.float64),
+                        terminated=np.zeros((e, n), np.uint8), truncated=np.zeros((e, n), np.uint8),
+                        env_done=np.zeros(e, np.uint8), dist_goal=np.zeros((e, n), np.float32),
+                        flags=np.zeros((e, n), np.uint8),
+                        global_state=np.zeros((e, 6 * n + 3), np.float32))
+        self.prm = make_params(cfg, e, auto_reset=True, seed=seed, env_offset=env_offset)
+        self._call(1, None)  # device-RNG reset of every env
+
+    def _call(self, mode: int, actions) -> None:
+        st, out = self.st, self.out
+        rc = lib().oracle_run(
+            ctypes.byref(self.prm), mode, _p(st["pos"]), _p(st["vel"]), _p(st["goal"]),
+            _p(st["obst"]) if st["obst"].size else None, _p(st["active"]), _p(st["step"]),
+            _p(st["episode"]), _p(st["damping"]), _p(actions), None, None, _p(out["obs"]),
+            _p(out["reward"]), _p(out["terminated"]), _p(out["truncated"]), _p(out["env_done"]),
+            _p(out["dist_goal"]), _p(out["flags"]), _p(out["global_state"]), self.nthreads)
+        if rc != 0:
+            raise RuntimeError("oracle_run failed")
+
+    def step(self, actions: np.ndarray) -> None:
+        self._call(0, np.ascontiguousarray(actions, np.float32))

@@ -1,0 +1,113 @@
+"""CPU, world_size 2 over gloo: bench.py's multi-rank logic with CPU stand-in steps.
+
+The same functions bench.main() uses on the GPU (shard_plan, timed_region, max_over_ranks,
+gather_schedule + the CTDE all_gather_into_tensor) drive a C-oracle stand-in for the step on
+each rank.  Checks: the weak-scaling shards equal one run over the whole batch (the reset RNG is
+keyed by the global env index), every rank sees the MAX of the per-rank timings, and the
+periodic global_state gather concatenates the shards in rank order at the scheduled steps.
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+N, E_PER, STEPS, EVERY = 5, 6, 7, 3
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _actions(world: int, t: int) -> np.ndarray:
+    return np.random.default_rng(500 + t).uniform(-1, 1, (world * E_PER, N, 3)).astype(np.float32)
+
+
+def _worker(rank: int, world: int, port: int, outdir: str) -> None:
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from oracle import c_oracle as co
+        from oracle import swarm_oracle as so
+        off, cnt = bench.shard_plan(world, rank, E_PER)
+        cfg = so.make_cfg(num_drones=N, max_steps=4)
+        run = co.Runner(cfg, cnt, seed=9, env_offset=off, nthreads=1)
+        sched = set(bench.gather_schedule(STEPS, EVERY))
+        buf = torch.empty((world * cnt, 6 * N + 3))
+        gathered, obs = {}, []
+
+        def body():
+            for k in range(STEPS):
+                run.step(_actions(world, k)[off:off + cnt])
+                obs.append(run.out["obs"].copy())
+                if k in sched:
+                    dist.all_gather_into_tensor(buf, torch.from_numpy(run.out["global_state"]))
+                    gathered[k] = buf.numpy().copy()
+        wall = bench.timed_region(body, world, lambda: None)
+        # rank-dependent stand-in timings: every rank must get the max
+        m = bench.max_over_ranks([wall, 1.0 + rank, 10.0 - rank], world)
+        np.savez(os.path.join(outdir, f"r{rank}.npz"), obs=np.stack(obs), off=off, cnt=cnt,
+                 m=np.array(m), gk=np.array(sorted(gathered)),
+                 g=np.stack([gathered[k] for k in sorted(gathered)]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_bench_rank_logic_gloo(tmp_path):
+    import bench
+    from oracle import c_oracle as co
+    from oracle import swarm_oracle as so
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    cfg = so.make_cfg(num_drones=N, max_steps=4)
+    run = co.Runner(cfg, world * E_PER, seed=9, nthreads=1)
+    ref_obs, ref_gs = [], {}
+    sched = bench.gather_schedule(STEPS, EVERY)
+    for k in range(STEPS):
+        run.step(_actions(world, k))
+        ref_obs.append(run.out["obs"].copy())
+        if k in sched:
+            ref_gs[k] = run.out["global_state"].copy()
+    ref_obs = np.stack(ref_obs)
+    assert np.any(run.st["episode"] > 0), "the run should cross episode boundaries"
+    for r in range(world):
+        d = np.load(tmp_path / f"r{r}.npz")
+        off, cnt = int(d["off"]), int(d["cnt"])
+        assert (off, cnt) == (r * E_PER, E_PER)
+        assert np.array_equal(d["obs"], ref_obs[:, off:off + cnt]), f"rank {r} obs"
+        assert d["m"][1] == 1.0 + (world - 1) and d["m"][2] == 10.0, "max over ranks"
+        assert d["gk"].tolist() == sched
+        for i, k in enumerate(sched):
+            assert np.array_equal(d["g"][i], ref_gs[k]), f"rank {r} gathered global_state @ {k}"
+
+
+def test_gather_schedule_and_shards():
+    import bench
+    assert bench.gather_schedule(7, 3) == [2, 5, 6]
+    assert bench.gather_schedule(6, 3) == [2, 5]
+    assert bench.gather_schedule(5, 8) == [4]
+    assert bench.shard_plan(8, 3, 8192) == (3 * 8192, 8192)
+    with pytest.raises(ValueError):
+        bench.shard_plan(2, 2, 10)
+
+
+def test_bench_args_presets():
+    import bench
+    a = bench.parse([])
+    assert (a.drones, a.envs, a.ctde) == (64, 8192, False)
+    a = bench.parse(["--config", "n16"])
+    assert (a.drones, a.envs, a.ctde) == (16, 1024, False)
+    a = bench.parse(["--config", "n256"])
+    assert (a.drones, a.envs, a.ctde) == (256, 1024, True)
+    a = bench.parse(["--config", "n256", "--envs", "64"])
+    assert a.envs == 64

@@ -12,6 +12,6 @@ for name in "$@"; do
     SWARM_MI355X_LIB=$so timeout -k 10 120 python bench.py --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/var/$name.log 2>&1
   fi
   rc=$?
-  echo "== $name rc=$rc $(grep -o '"kernel_ms_mean": [0-9.]*' gpurun_out/var/$name.log)"
+  echo "== $name rc=$rc $(grep -o "\"kernel_ms_mean\": [0-9.]*" gpurun_out/var/$name.log) $(grep -o "\"ms_per_step\": [0-9.]*" gpurun_out/var/$name.log)"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -5 gpurun_out/var/$name.log; exit $rc; fi
 done
