@@ -43,6 +43,7 @@ sys.path.insert(0, str(ROOT))
 METRIC = "agent-steps/sec at N=64 × E=8192 envs, 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 VALU_PEAK_LANE_OPS = 78.6e12  # f32 VALU lane-ops/s (157.3 TFLOP/s counting FMA as 2); SURVEY §8d
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA peaks, MI355X_MICROARCH.md
 
 # BASELINE.json configs, per GPU: [2] is the headline (the metric's config), [1] and [4] have
 # their own bench lines (profiles/r02_config_lines.jsonl).
@@ -80,6 +81,9 @@ def parse(argv=None):
                     help="time the whole-job rate with eager launches instead of hipGraph replay")
     ap.add_argument("--ctde", action="store_true", default=None,
                     help="also emit global_state and all-gather it (config 5)")
+    ap.add_argument("--policy", choices=("bf16", "f32"), default=None,
+                    help="rollout mode: each step = on-device actor inference on the obs tensor "
+                         "(swarm_policy_forward, random-init TorchFC 256x256 weights) + the env step")
     ap.add_argument("--gather-every", type=int, default=8,
                     help="CTDE all-gather period in steps (SURVEY.md §5: per batch, not per step)")
     a = ap.parse_args(argv)
@@ -244,14 +248,31 @@ def main(argv=None):
     vec.reset()
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     ring = [torch.rand((e, n, 3), device=dev, generator=gen) * 2 - 1 for _ in range(args.ring)]
+    pol, pol_act = None, None
+    if args.policy:
+        from swarm_marl_amd.policy import PolicyMLP
+        rng = np.random.default_rng(7)  # random-init weights of the reference architecture
+        d = vec.obs_dim
+        pol = PolicyMLP.from_arrays(rng.normal(0, d ** -0.5, (256, d)), np.zeros(256),
+                                    rng.normal(0, 256 ** -0.5, (256, 256)), np.zeros(256),
+                                    rng.normal(0, 0.01, (6, 256)), np.zeros(6), device=dev,
+                                    precision=args.policy)
+        pol_act = torch.zeros((e, n, 3), device=dev)
     gather_buf = None
     gathers = set()
     if args.ctde and world > 1:
         gather_buf = torch.empty((world * e, 6 * n + 3), device=dev)
         gathers = set(gather_schedule(args.steps, args.gather_every))
 
+    def env_step(k):
+        if pol is not None:  # rollout: actions from the policy on the current obs, in place
+            pol.act(vec.obs, out=pol_act)
+            vec.step(pol_act)
+        else:
+            vec.step(ring[k % args.ring])
+
     def step(k):
-        vec.step(ring[k % args.ring])
+        env_step(k)
         if gather_buf is not None and k in gathers:
             dist.all_gather_into_tensor(gather_buf, vec.global_state)
 
@@ -268,7 +289,7 @@ def main(argv=None):
         # thread_local: the RCCL watchdog thread of a multi-rank run keeps querying its events
         with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             for k in range(args.ring):
-                vec.step(ring[k])
+                env_step(k)
         graph.replay()  # untimed
         reps, rem = divmod(args.steps, args.ring)
 
@@ -277,9 +298,10 @@ def main(argv=None):
             for _ in range(reps):
                 graph.replay()
             for k in range(rem):
-                vec.step(ring[k])
+                env_step(k)
             t_ev[1].record(stream)
-        timing = f"hipGraph replay of {args.ring}-step segments"
+        timing = f"hipGraph replay of {args.ring}-step segments" + (
+            f" (policy {args.policy} + env step per step)" if pol is not None else "")
     else:
         def body():
             t_ev[0].record(stream)
@@ -298,13 +320,23 @@ def main(argv=None):
     def body_eager():
         for k in range(args.steps):
             ev[k][0].record(stream)
-            vec.step(ring[k % args.ring])
+            env_step(k)
             ev[k][1].record(stream)
     wall_eager = timed_region(body_eager, world, sync)
     kern_eager = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
-    wall_max, kern_max, eager_max, kern_eager_max = max_over_ranks(
-        [wall, kern_ms, wall_eager, kern_eager], world, dev)
+    pol_ms = 0.0
+    if pol is not None:  # the policy kernel alone, K launches on the current obs, events around them
+        pe = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        sync()
+        pe[0].record(stream)
+        for _ in range(args.steps):
+            pol.act(vec.obs, out=pol_act)
+        pe[1].record(stream)
+        sync()
+        pol_ms = pe[0].elapsed_time(pe[1]) / args.steps
+    wall_max, kern_max, eager_max, kern_eager_max, pol_max = max_over_ranks(
+        [wall, kern_ms, wall_eager, kern_eager, pol_ms], world, dev)
     done_frac = float((vec.env_done != 0).float().mean())
 
     if rank == 0:
@@ -333,8 +365,10 @@ def main(argv=None):
                             "peak": VALU_PEAK_LANE_OPS,
                             "frac": lane_ops / (kern_max * 1e-3) / VALU_PEAK_LANE_OPS,
                             "source": "SQ_INSTS_VALU x 64 lanes from profiles/pmc_traffic.json"}
+        metric = METRIC if pol is None else \
+            "rollout agent-steps/sec (on-device policy + env step) at N=64 x E=8192 per MI355X"
         rec = {
-            "metric": METRIC, "value": value, "unit": "agent-steps/s", "n_gpus": world,
+            "metric": metric, "value": value, "unit": "agent-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall_max / args.steps * 1e3,
             "ms_per_step_eager": eager_max / args.steps * 1e3, "step_timing": timing,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
@@ -351,6 +385,18 @@ def main(argv=None):
             "roofline": roof,
             "env_done_fraction_last_step": done_frac,
         }
+        if pol is not None:
+            rows = e * n
+            flops = 2.0 * rows * (pol.in_dim * 256 + 256 * 256 + 256 * pol.out_dim)
+            tf = flops / (pol_max * 1e-3) / 1e12
+            rec["policy"] = {"precision": args.policy, "kernel": f"policy_mlp_{args.policy}",
+                             "rows_per_launch": rows, "algorithmic_flops_per_launch": flops,
+                             "kernel_ms_mean": pol_max,
+                             "roofline": {"bound": "mfma", "achieved": tf,
+                                          "peak": MFMA_PEAK_TFLOPS[args.policy], "unit": "TFLOP/s",
+                                          "frac": tf / MFMA_PEAK_TFLOPS[args.policy]},
+                             "weights": "random-init TorchFC [256, 256] relu (no checkpoint)"}
+            rec["roofline"]["note"] = "env-step roofline fields cover the whole rollout step"
         if not args.no_cpu_baseline and world == 1:
             rec["cpu_baseline"] = cpu_baseline_port(n, e, args.cpu_seconds, raw)
             if args.cpu_variant_seconds > 0 and not args.no_term:

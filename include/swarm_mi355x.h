@@ -198,6 +198,48 @@ int swarm_reset(const swarm_params_t* p, const swarm_state_t* s, const uint8_t* 
 int swarm_observe(const swarm_params_t* p, const swarm_state_t* s, const uint8_t* env_mask,
                   const swarm_out_t* o, void* hip_stream);
 
+
+/*
+ * On-device actor inference: the reference's exported policy
+ * (scripts/export_onnx.py:120-141: RLlib TorchFC, fcnet_hiddens [256, 256], relu;
+ * src/swarm_marl/training/config_builders.py:53-56, models.py:75-81)
+ *     logits = W3 relu(W2 relu(W1 x + b1) + b2) + b3,   logits = [mean | log_std]
+ * run on the GPU over the env's observation tensor, writing logits and/or the next actions
+ * (RLlib TorchDiagGaussian: deterministic = mean; sampled = mean + exp(log_std) * N(0, 1)).
+ * It replaces the policy forward the reference runs on the host per agent
+ * (algo.compute_single_action / the ONNX graph, scripts/evaluate_protocol.py:152-170).
+ */
+#define SWARM_POLICY_HIDDEN 256
+#define SWARM_POLICY_MAX_IN 47      /* obs dim (one pad column carries the layer-1 bias) */
+#define SWARM_POLICY_MAX_OUT 12     /* logits (2 x action dim) */
+#define SWARM_POLICY_BF16 0         /* v_mfma_f32_32x32x16_bf16: bf16 operands, f32 accumulation */
+#define SWARM_POLICY_F32 1          /* v_mfma_f32_16x16x4_f32: f32 operands and sums */
+#define SWARM_POLICY_ACT_MEAN 0     /* actions = mean (deterministic) */
+#define SWARM_POLICY_ACT_SAMPLE 1   /* actions = mean + exp(log_std) * N(0,1), Philox(seed; row, counter) */
+
+typedef struct swarm_policy {
+  int32_t in_dim;        /* observation width D */
+  int32_t out_dim;       /* logits width (even) */
+  int32_t precision;     /* SWARM_POLICY_BF16 / SWARM_POLICY_F32 */
+  int32_t reserved;
+  const void* weights;   /* device copy of the swarm_policy_pack blob (16-B aligned) */
+} swarm_policy_t;
+
+/* Bytes of the packed weight blob (negative SWARM_E* code for unsupported dims). */
+long long swarm_policy_packed_bytes(int in_dim, int out_dim, int precision);
+
+/* Pack row-major f32 weights (PyTorch / ONNX Gemm transB layout: w1 [256,in], w2 [256,256],
+ * w3 [out,256]) into the kernel's fragment-order blob at host_out (host memory). */
+int swarm_policy_pack(int in_dim, int out_dim, int precision, const float* w1, const float* b1, const float* w2,
+                      const float* b2, const float* w3, const float* b3, void* host_out);
+
+/* logits [rows,out] (nullable) and/or actions [rows,out/2] (nullable) for obs [rows,in]; async on
+ * hip_stream, no allocation, no sync. */
+int swarm_policy_forward(const swarm_policy_t* p, const float* obs, long long rows, float* logits, float* actions,
+                         int action_mode, unsigned long long seed, unsigned long long counter, void* hip_stream);
+
+const char* swarm_policy_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

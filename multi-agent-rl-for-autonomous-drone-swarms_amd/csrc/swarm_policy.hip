@@ -1,0 +1,486 @@
+// swarm_policy.hip — on-device actor inference for the swarm rollout loop (gfx950, MFMA).
+//
+// The reference's actor is RLlib's TorchFC with fcnet_hiddens [256, 256] and relu
+// (src/swarm_marl/training/config_builders.py:53-56, models.py:75-81), exported by
+// scripts/export_onnx.py:120-141 as  logits = Gemm(Relu(Gemm(Relu(Gemm(obs)))))  (transB = 1).
+// RLlib's TorchDiagGaussian reads logits = [mean | log_std]; its deterministic action is the mean.
+//
+// swarm_policy_forward runs that MLP over `rows` observation rows (E x N agents of a VecSwarm,
+// obs [E,N,D] read in place) and writes logits and/or actions [rows, out/2] (the env's action
+// tensor), so observations never leave HBM between env steps.
+//
+// bf16 path (default): v_mfma_f32_32x32x16_bf16, f32 accumulation.  One wave owns a tile of 32
+// obs rows and computes every layer TRANSPOSED, C[out][row] = W · X^T: the row index sits on
+// the lane, so a layer's f32 accumulators, relu'd and packed to bf16 in place, ARE the next
+// layer's B operand (no LDS round trip, no shuffles).  The k order of such an operand is the
+// accumulator's register order (element j of lane half h in k-step s is row
+// 16s + 8(j>>2) + 4h + (j&3) of the 32-row block), so the host packs W2 / W3 with that
+// permutation of their input index.  Weights live in LDS in MFMA-fragment order (one 1-KB block
+// of 64 lanes x 16 B per (out block, k step): every A read is one conflict-free ds_read_b128);
+// the layer-1 bias rides in the pad column k = D of the obs fragment (x[D] = 1).
+// f32 path: v_mfma_f32_16x16x4_f32 (f32 products, f32 sums: within summation-order rounding of
+// the f32 graph) on 16-row tiles, the same accumulator-as-operand chaining; A fragments stream
+// from global memory (L2-resident, 256 B per wave-instruction).
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <string.h>
+
+#include "swarm_mi355x.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int H = SWARM_POLICY_HIDDEN;  // 256
+constexpr int KP1 = 48;                 // bf16 layer-1 K (obs dim + bias column, padded)
+constexpr int KS1 = KP1 / 16;           // 3 k-steps
+constexpr int OB = H / 32;              // 8 out blocks of 32 (bf16 path)
+constexpr int KS2 = H / 16;             // 16 k-steps over the hidden dim
+constexpr int FRAG = 1024;              // bytes of one 64-lane x 16-B fragment block
+
+// ---------------------------------------------------------------- packed blob layouts
+// bf16: [W1F 8x3 blocks][W2F 8x16 blocks][W3F 16 k-steps x 2*out lanes x 16 B][b2 256 f32][b3 32 f32]
+struct Bf16Layout {
+  int out;
+  size_t w1, w2, w3, b2, b3, total;
+  __host__ __device__ explicit Bf16Layout(int o) : out(o) {
+    w1 = 0;
+    w2 = w1 + (size_t)OB * KS1 * FRAG;
+    w3 = w2 + (size_t)OB * KS2 * FRAG;
+    b2 = w3 + (size_t)KS2 * 2 * o * 16;
+    b3 = b2 + H * 4;
+    total = b3 + 32 * 4;
+  }
+};
+// f32: [W1 16 obs x KQ1 q x 64 lanes][W2 16 x 64 x 64][W3 64 x 64][b2 256][b3 16] floats
+struct F32Layout {
+  int kq1;
+  size_t w1, w2, w3, b2, b3, total;  // float offsets
+  __host__ __device__ explicit F32Layout(int in) {
+    kq1 = (in + 1 + 3) / 4;
+    w1 = 0;
+    w2 = w1 + (size_t)16 * kq1 * 64;
+    w3 = w2 + (size_t)16 * 64 * 64;
+    b2 = w3 + (size_t)64 * 64;
+    b3 = b2 + H;
+    total = b3 + 16;
+  }
+};
+
+// hidden unit carried by k-step `ks` (of 16) of an accumulator-chained operand, lane half h, element j
+__host__ __device__ inline int chained_k(int ks, int h, int j) {
+  return (ks >> 1) * 32 + 16 * (ks & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
+}
+// f32 16x16x4 chaining: k-step q (of 64) of lane quarter g -> hidden unit
+__host__ __device__ inline int chained_k_f32(int q, int g) { return (q >> 2) * 16 + 4 * g + (q & 3); }
+
+uint16_t bf16_rne(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// ---------------------------------------------------------------- bf16 kernel
+__device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
+
+__device__ __forceinline__ bf16x8 pack8(const f32x16& a, int s, bool act) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)(act ? relu(a[8 * s + j]) : a[8 * s + j]);
+  return r;
+}
+
+// Philox4x32-10 (same constants as the env's device reset)
+__device__ __forceinline__ void philox(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[0] = n0; c[1] = (uint32_t)p1; c[2] = n2; c[3] = (uint32_t)p0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+
+struct FwdArgs {
+  const void* w;        // packed blob (device)
+  const float* obs;     // [rows, in]
+  float* logits;        // [rows, out] or null
+  float* actions;       // [rows, out/2] or null
+  long long rows;
+  int in, out, mode;    // mode: 0 mean, 1 sample
+  uint32_t seed_lo, seed_hi, ctr_lo, ctr_hi;
+};
+
+template <int WAVES, int MODE>
+__global__ void __launch_bounds__(64 * WAVES) policy_mlp_bf16(const FwdArgs A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const Bf16Layout L(A.out);
+  {  // stage the packed weights in LDS (once per workgroup)
+    const int4* src = reinterpret_cast<const int4*>(A.w);
+    int4* dst = reinterpret_cast<int4*>(lds);
+    const int n16 = (int)(L.total / 16);
+    for (int i = threadIdx.x; i < n16; i += 64 * WAVES) dst[i] = src[i];
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6;
+  const long long ntiles = (A.rows + 31) / 32;
+  const float* b2 = reinterpret_cast<const float*>(lds + L.b2);
+  const float* b3 = reinterpret_cast<const float*>(lds + L.b3);
+  for (long long tile = (long long)blockIdx.x * WAVES + wave; tile < ntiles; tile += (long long)gridDim.x * WAVES) {
+    // Opaque per tile: the lane index and the layer dims.  Everything derived from them (fragment
+    // addresses, the obs element offsets and their pad/bias selects, the layer-3 row masks) is
+    // recomputed per tile instead of being hoisted out of the loop, where it would stay live
+    // next to h1/h2 (64 + 64 VGPRs) and spill.
+    int lane = threadIdx.x & 63, in = A.in, out = A.out;
+    asm volatile("" : "+v"(lane), "+s"(in), "+s"(out));
+    const int n = lane & 31, h = lane >> 5;
+    const bool w3lane = n < out;
+    const int w3idx = h * out + n;
+    const uint32_t lb = 16u * (uint32_t)lane;
+    const bf16x8* w1f = reinterpret_cast<const bf16x8*>(lds + L.w1 + lb);
+    const bf16x8* w2f = reinterpret_cast<const bf16x8*>(lds + L.w2 + lb);
+    const bf16x8* w3f = reinterpret_cast<const bf16x8*>(lds + L.w3);
+    const long long row = tile * 32 + n;
+    const bool valid = row < A.rows;
+    // ---- obs fragments (B of layer 1): x[row][16 ks + 8 h + j], x[in] = 1 (bias column).
+    // Unconditional loads from clamped addresses (one wait for all of them), then selects.
+    const float* xr = A.obs + (valid ? row : A.rows - 1) * in;
+    float xv[KS1 * 8];
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 16 * ks + 8 * h + j;
+        xv[ks * 8 + j] = xr[k < in ? k : in - 1];
+      }
+    bf16x8 xb[KS1];
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 16 * ks + 8 * h + j;
+        xb[ks][j] = (__bf16)(k < in ? xv[ks * 8 + j] : (k == in ? 1.f : 0.f));
+      }
+    // ---- layer 1: 256 x (in + 1), relu -> h1 (16 k-step fragments)
+    bf16x8 h1[KS2];
+#pragma unroll
+    for (int ob = 0; ob < OB; ++ob) {
+      f32x16 acc = {};
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[(ob * KS1 + ks) * 64], xb[ks], acc, 0, 0, 0);
+      h1[2 * ob] = pack8(acc, 0, true);
+      h1[2 * ob + 1] = pack8(acc, 1, true);
+      __builtin_amdgcn_sched_barrier(0);  // keep each out block's fragment reads inside it
+    }
+    // ---- layer 2: 256 x 256, relu -> h2
+    bf16x8 h2[KS2];
+#pragma unroll
+    for (int ob = 0; ob < OB; ++ob) {
+      f32x16 acc;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 b = *reinterpret_cast<const float4*>(b2 + ob * 32 + 8 * g + 4 * h);
+        acc[4 * g + 0] = b.x; acc[4 * g + 1] = b.y; acc[4 * g + 2] = b.z; acc[4 * g + 3] = b.w;
+      }
+#pragma unroll
+      for (int ks = 0; ks < KS2; ++ks) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2f[(ob * KS2 + ks) * 64], h1[ks], acc, 0, 0, 0);
+        if ((ks & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // <= 8 fragments (32 VGPRs) in flight
+      }
+      h2[2 * ob] = pack8(acc, 0, true);
+      h2[2 * ob + 1] = pack8(acc, 1, true);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- layer 3: out x 256 (rows >= out are zero fragments)
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
+      acc[i] = m < out ? b3[m] : 0.f;
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS2; ++ks) {
+      bf16x8 a = {};
+      if (w3lane) a = w3f[ks * 2 * out + w3idx];
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, h2[ks], acc, 0, 0, 0);
+    }
+    // ---- outputs: lane holds logits m = (i&3) + 8(i>>2) + 4h of its row (out <= 12: i < 8)
+    if (A.logits && valid) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (m < out) A.logits[row * out + m] = acc[i];
+      }
+    }
+    if (A.actions) {
+      // gather the row's logits 0..out-1 on the lane pair (n, n + 32): half 0 holds m 0-3, 8-11;
+      // half 1 holds m 4-7
+      float lg[12];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float mine = acc[i];
+        const float other = __shfl_xor(mine, 32);
+        const int m_me = (i & 3) + 8 * (i >> 2) + 4 * h, m_ot = (i & 3) + 8 * (i >> 2) + 4 * (1 - h);
+        if (m_me < 12) lg[m_me] = mine;
+        if (m_ot < 12) lg[m_ot] = other;
+      }
+      const int ad = out / 2;
+      if (h == 0 && valid) {
+        float z[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if constexpr (MODE == SWARM_POLICY_ACT_SAMPLE) {  // Box-Muller normals from Philox(seed; row, counter)
+          uint32_t c[4] = {(uint32_t)row, (uint32_t)((unsigned long long)row >> 32), A.ctr_lo, A.ctr_hi};
+          philox(c, A.seed_lo, A.seed_hi);
+          uint32_t c2[4] = {(uint32_t)row, (uint32_t)((unsigned long long)row >> 32) ^ 0x80000000u, A.ctr_lo, A.ctr_hi};
+          if (ad > 2) philox(c2, A.seed_lo, A.seed_hi);
+          const uint32_t u[8] = {c[0], c[1], c[2], c[3], c2[0], c2[1], c2[2], c2[3]};
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            const float u1 = ((float)(u[2 * p] >> 8) + 0.5f) * 0x1p-24f;
+            const float u2 = (float)(u[2 * p + 1] >> 8) * 0x1p-24f;
+            const float r = sqrtf(-2.f * logf(u1));
+            z[2 * p] = r * cosf(6.28318530717958647692f * u2);
+            z[2 * p + 1] = r * sinf(6.28318530717958647692f * u2);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          if (k < ad) {
+            float a = lg[k];
+            if constexpr (MODE == SWARM_POLICY_ACT_SAMPLE) a = a + expf(lg[ad + k]) * z[k];
+            A.actions[row * ad + k] = a;
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- f32 kernel (16-row tiles)
+// A fragments are read with buffer loads: one lane-offset VGPR for every load of a tile, the
+// fragment's byte offset in an SGPR (per-lane 64-bit addresses for ~1,200 distinct fragments
+// would be hoisted out of the tile loop and spilled).
+constexpr int BUF_DWORD3 = 0x00020000;  // gfx9 raw buffer descriptor word 3
+__device__ __forceinline__ float wload(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t sbase, uint32_t soff_floats) {
+  return __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)(sbase + soff_floats * 4u), 0));
+}
+
+template <int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) policy_mlp_f32(const FwdArgs A) {
+  const F32Layout L(A.in);
+  const __amdgpu_buffer_rsrc_t W =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(A.w), 0, (int)(L.total * 4), BUF_DWORD3);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = lane & 15, g = lane >> 4;
+  const long long ntiles = (A.rows + 15) / 16;
+  const int in = A.in, out = A.out, kq1 = L.kq1;
+  for (long long tile = (long long)blockIdx.x * WAVES + wave; tile < ntiles; tile += (long long)gridDim.x * WAVES) {
+    uint32_t voff = 4u * (uint32_t)lane, sb = 0;
+    // opaque per tile: neither the lane offset nor the ~1,200 fragment offsets (SGPR soffset =
+    // sb + constant) are hoisted out of the tile loop, where they would be live and spill
+    asm volatile("" : "+v"(voff), "+s"(sb));
+    const long long row = tile * 16 + n;
+    const bool valid = row < A.rows;
+    const float* xr = A.obs + (valid ? row : 0) * in;
+    // ---- layer 1
+    f32x4 h1[16];
+#pragma unroll
+    for (int ob = 0; ob < 16; ++ob) h1[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < kq1; ++q) {
+      const int k = 4 * q + g;
+      const float x = k < in ? (valid ? xr[k] : 0.f) : (k == in ? 1.f : 0.f);
+#pragma unroll
+      for (int ob = 0; ob < 16; ++ob)
+        h1[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(wload(W, voff, sb, (uint32_t)(L.w1 + ((size_t)ob * kq1 + q) * 64)), x,
+                                                      h1[ob], 0, 0, 0);
+    }
+#pragma unroll
+    for (int ob = 0; ob < 16; ++ob)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h1[ob][i] = relu(h1[ob][i]);
+    // ---- layer 2
+    f32x4 h2[16];
+#pragma unroll
+    for (int ob = 0; ob < 16; ++ob) {
+      f32x4 acc;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = wload(W, 4u * (uint32_t)(4 * g + i), sb, (uint32_t)(L.b2 + ob * 16));
+#pragma unroll
+      for (int q = 0; q < 64; ++q) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wload(W, voff, sb, (uint32_t)(L.w2 + ((size_t)ob * 64 + q) * 64)),
+                                                   h1[q >> 2][q & 3], acc, 0, 0, 0);
+        if ((q & 15) == 15) __builtin_amdgcn_sched_barrier(0);  // at most 16 fragment loads in flight
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = relu(acc[i]);
+      h2[ob] = acc;
+    }
+    // ---- layer 3 (out <= 16)
+    f32x4 acc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = (4 * g + i) < out ? wload(W, 4u * (uint32_t)(4 * g + i), sb, (uint32_t)L.b3) : 0.f;
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wload(W, voff, sb, (uint32_t)(L.w3 + (size_t)q * 64)), h2[q >> 2][q & 3],
+                                                 acc, 0, 0, 0);
+      if ((q & 15) == 15) __builtin_amdgcn_sched_barrier(0);
+    }
+    // lane holds logits m = 4g + i of its row
+    if (A.logits && valid) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (4 * g + i < out) A.logits[row * out + 4 * g + i] = acc[i];
+    }
+    if (A.actions && valid) {
+      const int ad = out / 2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (4 * g + i < ad) A.actions[row * ad + 4 * g + i] = acc[i];
+    }
+  }
+}
+
+constexpr int BF16_WAVES = 8;
+constexpr int F32_WAVES = 4;
+
+thread_local char g_perr[256] = "";
+int pfail(int code, const char* msg) {
+  strncpy(g_perr, msg, sizeof(g_perr) - 1);
+  return code;
+}
+
+int grid_for(int waves_per_block, long long tiles) {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+      (void)hipGetLastError();
+      cus = 256;
+    }
+  }
+  long long need = (tiles + waves_per_block - 1) / waves_per_block;
+  long long g = need < cus ? need : cus;
+  return g < 1 ? 1 : (int)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* swarm_policy_last_error(void) { return g_perr; }
+
+long long swarm_policy_packed_bytes(int in_dim, int out_dim, int precision) {
+  if (in_dim < 1 || in_dim > SWARM_POLICY_MAX_IN || out_dim < 2 || out_dim > SWARM_POLICY_MAX_OUT || (out_dim & 1))
+    return pfail(SWARM_ELIMIT, "policy dims out of range"), (long long)SWARM_ELIMIT;
+  if (precision == SWARM_POLICY_BF16) return (long long)Bf16Layout(out_dim).total;
+  if (precision == SWARM_POLICY_F32) return (long long)F32Layout(in_dim).total * 4;
+  return pfail(SWARM_EINVAL, "unknown precision"), (long long)SWARM_EINVAL;
+}
+
+int swarm_policy_pack(int in_dim, int out_dim, int precision, const float* w1, const float* b1, const float* w2,
+                      const float* b2, const float* w3, const float* b3, void* host_out) {
+  const long long nb = swarm_policy_packed_bytes(in_dim, out_dim, precision);
+  if (nb < 0) return (int)nb;
+  if (!w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !host_out) return pfail(SWARM_ENULL, "null weight pointer");
+  memset(host_out, 0, (size_t)nb);
+  if (precision == SWARM_POLICY_BF16) {
+    const Bf16Layout L(out_dim);
+    unsigned char* base = static_cast<unsigned char*>(host_out);
+    uint16_t* w1f = reinterpret_cast<uint16_t*>(base + L.w1);
+    uint16_t* w2f = reinterpret_cast<uint16_t*>(base + L.w2);
+    uint16_t* w3f = reinterpret_cast<uint16_t*>(base + L.w3);
+    for (int ob = 0; ob < OB; ++ob)
+      for (int l = 0; l < 64; ++l) {
+        const int m = ob * 32 + (l & 31), h = l >> 5;
+        for (int ks = 0; ks < KS1; ++ks)
+          for (int j = 0; j < 8; ++j) {
+            const int k = 16 * ks + 8 * h + j;
+            const float v = k < in_dim ? w1[m * in_dim + k] : (k == in_dim ? b1[m] : 0.f);
+            w1f[((ob * KS1 + ks) * 64 + l) * 8 + j] = bf16_rne(v);
+          }
+        for (int ks = 0; ks < KS2; ++ks)
+          for (int j = 0; j < 8; ++j)
+            w2f[((ob * KS2 + ks) * 64 + l) * 8 + j] = bf16_rne(w2[m * H + chained_k(ks, h, j)]);
+      }
+    for (int ks = 0; ks < KS2; ++ks)
+      for (int h = 0; h < 2; ++h)
+        for (int m = 0; m < out_dim; ++m)
+          for (int j = 0; j < 8; ++j)
+            w3f[((ks * 2 * out_dim) + h * out_dim + m) * 8 + j] = bf16_rne(w3[m * H + chained_k(ks, h, j)]);
+    memcpy(base + L.b2, b2, H * 4);
+    memcpy(base + L.b3, b3, (size_t)out_dim * 4);
+  } else {
+    const F32Layout L(in_dim);
+    float* f = static_cast<float*>(host_out);
+    for (int ob = 0; ob < 16; ++ob)
+      for (int l = 0; l < 64; ++l) {
+        const int m = ob * 16 + (l & 15), g = l >> 4;
+        for (int q = 0; q < L.kq1; ++q) {
+          const int k = 4 * q + g;
+          f[L.w1 + ((size_t)ob * L.kq1 + q) * 64 + l] = k < in_dim ? w1[m * in_dim + k] : (k == in_dim ? b1[m] : 0.f);
+        }
+        for (int q = 0; q < 64; ++q) f[L.w2 + ((size_t)ob * 64 + q) * 64 + l] = w2[m * H + chained_k_f32(q, g)];
+      }
+    for (int l = 0; l < 64; ++l) {
+      const int m = l & 15, g = l >> 4;
+      for (int q = 0; q < 64; ++q) f[L.w3 + (size_t)q * 64 + l] = m < out_dim ? w3[m * H + chained_k_f32(q, g)] : 0.f;
+    }
+    memcpy(f + L.b2, b2, H * 4);
+    memcpy(f + L.b3, b3, (size_t)out_dim * 4);
+  }
+  return SWARM_OK;
+}
+
+int swarm_policy_forward(const swarm_policy_t* p, const float* obs, long long rows, float* logits, float* actions,
+                         int action_mode, unsigned long long seed, unsigned long long counter, void* hip_stream) {
+  if (!p || !p->weights) return pfail(SWARM_ENULL, "policy/weights is NULL");
+  if (swarm_policy_packed_bytes(p->in_dim, p->out_dim, p->precision) < 0) return SWARM_ELIMIT;
+  if (rows < 0) return pfail(SWARM_EINVAL, "rows < 0");
+  if (rows == 0) return SWARM_OK;
+  if (!obs) return pfail(SWARM_ENULL, "obs is NULL");
+  if (!logits && !actions) return pfail(SWARM_ENULL, "need logits and/or actions");
+  if (action_mode != SWARM_POLICY_ACT_MEAN && action_mode != SWARM_POLICY_ACT_SAMPLE)
+    return pfail(SWARM_EINVAL, "unknown action_mode");
+  if (action_mode == SWARM_POLICY_ACT_SAMPLE && p->precision != SWARM_POLICY_BF16)
+    return pfail(SWARM_EINVAL, "sampled actions are implemented on the bf16 path");
+  if (((uintptr_t)p->weights) % 16) return pfail(SWARM_EINVAL, "weights must be 16-B aligned");
+  FwdArgs a;
+  a.w = p->weights;
+  a.obs = obs;
+  a.logits = logits;
+  a.actions = actions;
+  a.rows = rows;
+  a.in = p->in_dim;
+  a.out = p->out_dim;
+  a.mode = action_mode;
+  a.seed_lo = (uint32_t)seed;
+  a.seed_hi = (uint32_t)(seed >> 32);
+  a.ctr_lo = (uint32_t)counter;
+  a.ctr_hi = (uint32_t)(counter >> 32);
+  hipStream_t s = (hipStream_t)hip_stream;
+  if (p->precision == SWARM_POLICY_BF16) {
+    const int lds = (int)Bf16Layout(p->out_dim).total;
+    auto fn = action_mode == SWARM_POLICY_ACT_SAMPLE ? policy_mlp_bf16<BF16_WAVES, SWARM_POLICY_ACT_SAMPLE>
+                                                     : policy_mlp_bf16<BF16_WAVES, SWARM_POLICY_ACT_MEAN>;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+        hipSuccess)
+      return pfail(SWARM_EHIP, "hipFuncSetAttribute failed");
+    const int grid = grid_for(BF16_WAVES, (rows + 31) / 32);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * BF16_WAVES), lds, s, a);
+  } else {
+    const int grid = grid_for(F32_WAVES, (rows + 15) / 16) * 2;
+    hipLaunchKernelGGL(policy_mlp_f32<F32_WAVES>, dim3(grid), dim3(64 * F32_WAVES), 0, s, a);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return pfail(SWARM_EHIP, hipGetErrorString(e));
+  return SWARM_OK;
+}
+
+}  // extern "C"

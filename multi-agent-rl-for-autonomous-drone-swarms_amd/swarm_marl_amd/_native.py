@@ -43,10 +43,19 @@ AGENT_REACHED = 2
 AGENT_COLLISION = 4
 AGENT_HAS_OBS = 8
 
+POLICY_HIDDEN = 256
+POLICY_MAX_IN = 47
+POLICY_MAX_OUT = 12
+POLICY_BF16 = 0
+POLICY_F32 = 1
+POLICY_ACT_MEAN = 0
+POLICY_ACT_SAMPLE = 1
+
 # every symbol include/swarm_mi355x.h declares
 EXPORTED_SYMBOLS = (
     "swarm_abi_version", "swarm_last_error", "swarm_params_default", "swarm_obs_dim",
     "swarm_query_launch", "swarm_step", "swarm_reset", "swarm_observe",
+    "swarm_policy_packed_bytes", "swarm_policy_pack", "swarm_policy_forward", "swarm_policy_last_error",
 )
 
 
@@ -104,6 +113,11 @@ class SwarmOut(ctypes.Structure):
                  "info_flags", "global_state")]
 
 
+class SwarmPolicy(ctypes.Structure):
+    _fields_ = [("in_dim", ctypes.c_int32), ("out_dim", ctypes.c_int32), ("precision", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("weights", ctypes.c_void_p)]
+
+
 class SwarmLaunchInfo(ctypes.Structure):
     _fields_ = [(name, ctypes.c_int32) for name in
                 ("threads_per_block", "envs_per_block", "lanes_per_env", "blocks", "lds_bytes",
@@ -144,6 +158,16 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.swarm_reset.argtypes = [P, S, vp, O, vp]
     lib.swarm_observe.restype = ctypes.c_int
     lib.swarm_observe.argtypes = [P, S, vp, O, vp]
+    fp = ctypes.POINTER(ctypes.c_float)
+    lib.swarm_policy_packed_bytes.restype = ctypes.c_longlong
+    lib.swarm_policy_packed_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.swarm_policy_pack.restype = ctypes.c_int
+    lib.swarm_policy_pack.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, fp, fp, fp, fp, fp, fp, vp]
+    lib.swarm_policy_forward.restype = ctypes.c_int
+    lib.swarm_policy_forward.argtypes = [ctypes.POINTER(SwarmPolicy), vp, ctypes.c_longlong, vp, vp, ctypes.c_int,
+                                         ctypes.c_ulonglong, ctypes.c_ulonglong, vp]
+    lib.swarm_policy_last_error.restype = ctypes.c_char_p
+    lib.swarm_policy_last_error.argtypes = []
     got = lib.swarm_abi_version()
     if got != ABI_VERSION:
         raise NativeLibraryError(f"{p}: ABI version {got}, expected {ABI_VERSION}")
@@ -152,12 +176,13 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     return lib
 
 
-def check(rc: int, lib: ctypes.CDLL | None = None) -> None:
+def check(rc: int, lib: ctypes.CDLL | None = None, policy: bool = False) -> None:
     """Raise on a negative return code (bad arguments -> ValueError, HIP errors -> RuntimeError)."""
     if rc == SWARM_OK:
         return
     lib = lib or load_library()
-    msg = (lib.swarm_last_error() or b"").decode(errors="replace")
+    err = lib.swarm_policy_last_error if policy else lib.swarm_last_error
+    msg = (err() or b"").decode(errors="replace")
     if rc in (SWARM_EINVAL, SWARM_ENULL, SWARM_ELIMIT):
         raise ValueError(f"swarm_mi355x error {rc}: {msg}")
     raise RuntimeError(f"swarm_mi355x error {rc}: {msg}")
