@@ -28,7 +28,7 @@ def lib(nat):
 
 def _declared():
     text = HEADER.read_text()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(swarm_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|long long|const char\*)\s+(swarm_\w+)\s*\(", text, re.M)))
 
 
 def test_header_symbols_are_exported(nat, lib):
