@@ -48,7 +48,7 @@ MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA peaks, MI355X_MI
 # BASELINE.json configs, per GPU: [2] is the headline (the metric's config), [1] and [4] have
 # their own bench lines (profiles/r02_config_lines.jsonl).
 PRESETS = {
-    "headline": dict(drones=64, envs=8192, ctde=False,
+    "headline": dict(drones=64, envs=8192, ctde=False, groups=2,
                      label="config 3: N=64 x E=8192 on 1 MI355X (headline); config 4 per GPU"),
     "n16": dict(drones=16, envs=1024, ctde=False,
                 label="config 2: N=16 x E=1024 on 1 MI355X (launch-latency-bound)"),
@@ -84,6 +84,12 @@ def parse(argv=None):
     ap.add_argument("--policy", choices=("bf16", "f32"), default=None,
                     help="rollout mode: each step = on-device actor inference on the obs tensor "
                          "(swarm_policy_forward, random-init TorchFC 256x256 weights) + the env step")
+    ap.add_argument("--device-warmup-ms", type=float, default=200.0,
+                    help="untimed graph replays for this long before the timed region, after the W "
+                         "warm-up steps (GPU clocks ramp over ~100 ms; reported in the JSON line)")
+    ap.add_argument("--groups", type=int, default=None,
+                    help="env groups per GPU, each stepped on its own HIP stream (VecSwarm groups=G); "
+                         "default 2 for the headline, 1 otherwise")
     ap.add_argument("--gather-every", type=int, default=8,
                     help="CTDE all-gather period in steps (SURVEY.md §5: per batch, not per step)")
     a = ap.parse_args(argv)
@@ -92,6 +98,12 @@ def parse(argv=None):
     a.envs = pre["envs"] if a.envs is None else a.envs
     a.ctde = pre["ctde"] if a.ctde is None else a.ctde
     a.label = pre["label"]
+    if a.groups is None:
+        a.groups = pre.get("groups", 1)
+    if a.groups < 1:
+        ap.error("--groups must be >= 1")
+    if a.ctde and a.groups > 1:
+        ap.error("--ctde gathers the whole batch's global_state: use --groups 1")
     if a.gather_every < 1:
         ap.error("--gather-every must be >= 1")
     return a
@@ -244,7 +256,7 @@ def main(argv=None):
         raw.update(collision_radius=0.0, obstacle_radius=0.0, goal_radius=0.0)
     vec = VecSwarm(e, raw, device=dev, auto_reset=True, seed=0, env_offset=offset,
                    with_global_state=args.ctde, persistent=not args.no_persistent,
-                   waves_per_simd=args.waves_per_simd)
+                   waves_per_simd=args.waves_per_simd, groups=args.groups)
     vec.reset()
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     ring = [torch.rand((e, n, 3), device=dev, generator=gen) * 2 - 1 for _ in range(args.ring)]
@@ -264,79 +276,171 @@ def main(argv=None):
         gather_buf = torch.empty((world * e, 6 * n + 3), device=dev)
         gathers = set(gather_schedule(args.steps, args.gather_every))
 
-    def env_step(k):
+    G = vec.groups
+    slices = vec.group_slices
+
+    def env_step_group(g, k):  # group g's step k on the current stream
         if pol is not None:  # rollout: actions from the policy on the current obs, in place
-            pol.act(vec.obs, out=pol_act)
-            vec.step(pol_act)
+            lo, hi = slices[g]
+            pol.act(vec.obs[lo:hi], out=pol_act[lo:hi])
+            vec.step_group(g, pol_act)
         else:
-            vec.step(ring[k % args.ring])
+            vec.step_group(g, ring[k % args.ring])
+
+    def env_step(k):  # whole batch: group g on group stream g (not joined: groups overlap)
+        if G == 1:
+            env_step_group(0, k)
+            return
+        for g, st in enumerate(vec.group_streams):
+            with torch.cuda.stream(st):
+                env_step_group(g, k)
 
     def step(k):
         env_step(k)
         if gather_buf is not None and k in gathers:
+            vec.join()
             dist.all_gather_into_tensor(gather_buf, vec.global_state)
 
-    for k in range(args.warmup):
-        step(k)
     stream = torch.cuda.current_stream(dev)
     sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+    for k in range(args.warmup):
+        step(k)
+    sync()
+
+    # With env groups the timed region is bracketed on group stream 0 (the other groups fork
+    # from and join into it): the null stream, which may share a hardware queue with a group
+    # stream, then carries no work inside the timed region.
+    if G > 1:
+        stream = vec.group_streams[0]
+
+    def fork(ev):  # the other group streams start after `ev` on the bracket stream
+        if G > 1:
+            for st in vec.group_streams[1:]:
+                st.wait_event(ev)
+
+    def join():
+        if G > 1:
+            for st in vec.group_streams[1:]:
+                stream.wait_stream(st)
 
     # ---- timed region: hipGraph replay of ring segments (or eager with --no-graph / CTDE)
+    # With env groups: one graph per group, captured and replayed on its group stream; the
+    # events on the launch stream fork to / join from the group streams, so they bracket the
+    # whole batch's K steps.
     t_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     use_graph = not args.no_graph and gather_buf is None
+    reps, rem = divmod(args.steps, args.ring)
     if use_graph:
-        graph = torch.cuda.CUDAGraph()
-        # thread_local: the RCCL watchdog thread of a multi-rank run keeps querying its events
-        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
-            for k in range(args.ring):
-                env_step(k)
-        graph.replay()  # untimed
-        reps, rem = divmod(args.steps, args.ring)
+        def capture(n_steps):  # one graph of n_steps ring steps per group, on its group stream
+            out = []
+            for g in range(G):
+                gr = torch.cuda.CUDAGraph()
+                # thread_local: the RCCL watchdog thread of a multi-rank run keeps querying its events
+                if G == 1:
+                    with torch.cuda.graph(gr, capture_error_mode="thread_local"):
+                        for k in range(n_steps):
+                            env_step_group(0, k)
+                else:
+                    st = vec.group_streams[g]
+                    with torch.cuda.stream(st), torch.cuda.graph(gr, stream=st, capture_error_mode="thread_local"):
+                        for k in range(n_steps):
+                            env_step_group(g, k)
+                out.append(gr)
+            return out
+        graphs = capture(args.ring)
+        tail = capture(rem) if rem else None  # the K % ring remainder, also replayed from a graph
+
+        def replay_all(gs):
+            if G == 1:
+                gs[0].replay()
+                return
+            for g, st in enumerate(vec.group_streams):
+                with torch.cuda.stream(st):
+                    gs[g].replay()
+        replay_all(graphs)  # untimed
+        sync()
 
         def body():
             t_ev[0].record(stream)
+            fork(t_ev[0])
             for _ in range(reps):
-                graph.replay()
-            for k in range(rem):
-                env_step(k)
+                replay_all(graphs)
+            if tail is not None:
+                replay_all(tail)
+            join()
             t_ev[1].record(stream)
         timing = f"hipGraph replay of {args.ring}-step segments" + (
+            f", {G} env groups on {G} HIP streams (one graph per group)" if G > 1 else "") + (
             f" (policy {args.policy} + env step per step)" if pol is not None else "")
     else:
         def body():
             t_ev[0].record(stream)
+            fork(t_ev[0])
             for k in range(args.steps):
                 step(k)
+            join()
             t_ev[1].record(stream)
-        timing = "eager launches" + (f", CTDE all-gather every {args.gather_every} steps"
-                                     if gather_buf is not None else "")
+        timing = "eager launches" + (f", {G} env groups on {G} HIP streams" if G > 1 else "") + (
+            f", CTDE all-gather every {args.gather_every} steps" if gather_buf is not None else "")
+    # device warm-up: untimed ring segments until the clocks have ramped (not part of W or K)
+    warm_ms, warm_steps = 0.0, 0
+    if args.device_warmup_ms > 0:
+        sync()
+        t0 = time.perf_counter()
+        # time-based unless a step holds a collective (every rank must then run the same count)
+        fixed = None if gather_buf is None else max(args.ring, int(args.device_warmup_ms * 5))
+        while ((time.perf_counter() - t0) * 1e3 < args.device_warmup_ms if fixed is None
+               else warm_steps < fixed):
+            if use_graph:
+                replay_all(graphs)
+                warm_steps += args.ring
+            else:
+                for k in range(args.ring):
+                    step(k)
+                warm_steps += args.ring
+            if warm_steps % (8 * args.ring) == 0:
+                sync()
+        sync()
+        warm_ms = (time.perf_counter() - t0) * 1e3
     wall = timed_region(body, world, sync)
     kern_ms = t_ev[0].elapsed_time(t_ev[1]) / args.steps
 
-    # ---- diagnostic pass: eager launches, one event pair around every launch
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    # ---- diagnostic pass: eager launches, one event pair around every launch on its stream
+    # (with env groups the launches of a step overlap: the per-launch mean is what rocprofv3
+    # reports per dispatch, the whole pass / K is the eager step time)
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)] for _ in range(G)]
+    ev_all = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    streams_g = vec.group_streams if G > 1 else [stream]
 
     def body_eager():
+        ev_all[0].record(stream)
+        fork(ev_all[0])
         for k in range(args.steps):
-            ev[k][0].record(stream)
-            env_step(k)
-            ev[k][1].record(stream)
+            for g, st in enumerate(streams_g):
+                with torch.cuda.stream(st):
+                    ev[g][k][0].record(st)
+                    env_step_group(g, k)
+                    ev[g][k][1].record(st)
+        join()
+        ev_all[1].record(stream)
     wall_eager = timed_region(body_eager, world, sync)
-    kern_eager = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_launch = float(np.mean([a.elapsed_time(b) for row in ev for a, b in row]))
+    kern_eager = ev_all[0].elapsed_time(ev_all[1]) / args.steps
 
     pol_ms = 0.0
     if pol is not None:  # the policy kernel alone, K launches on the current obs, events around them
         pe = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         sync()
-        pe[0].record(stream)
+        cs = torch.cuda.current_stream(dev)
+        pe[0].record(cs)
         for _ in range(args.steps):
             pol.act(vec.obs, out=pol_act)
-        pe[1].record(stream)
+        pe[1].record(cs)
         sync()
         pol_ms = pe[0].elapsed_time(pe[1]) / args.steps
-    wall_max, kern_max, eager_max, kern_eager_max, pol_max = max_over_ranks(
-        [wall, kern_ms, wall_eager, kern_eager, pol_ms], world, dev)
+    wall_max, kern_max, eager_max, kern_eager_max, launch_max, pol_max = max_over_ranks(
+        [wall, kern_ms, wall_eager, kern_eager, kern_launch, pol_ms], world, dev)
     done_frac = float((vec.env_done != 0).float().mean())
 
     if rank == 0:
@@ -354,11 +458,20 @@ def main(argv=None):
                                    f"measured in this run") if prof else None,
                 "algorithmic_bytes_per_launch": bytes_launch,
                 "kernel_ms_mean": kern_max,
-                "kernel_ms_timing": "HIP events on the launch stream around the timed region "
-                                    "(graph replays), / K; max over ranks",
+                "kernel_ms_timing": ("HIP events on the launch stream around the timed region "
+                                     "(graph replays), / K; max over ranks") if G == 1 else
+                                    (f"HIP events on the launch stream around the timed region, "
+                                     f"forked to and joined from the {G} group streams (graph "
+                                     f"replays), / K = whole-batch step time ({G} overlapping "
+                                     f"launches of E/{G} envs per step); max over ranks"),
                 "kernel_ms_eager_events": kern_eager_max,
+                "kernel_ms_per_launch": launch_max,
+                "kernel_ms_per_launch_timing": "eager pass, HIP events around each launch on its own "
+                                               "stream, mean (compare rocprofv3 per-dispatch average"
+                                               + (f"; the {G} launches of a step overlap" if G > 1 else "") + ")",
                 "kernel": vec.kernel_name(),
-                "grid": int(vec.launch_info.blocks)}
+                "grid": int(vec.group_launch_info[0].blocks),
+                "env_groups": G, "launches_per_step": G}
         if prof.get("valu_insts_per_launch"):
             lane_ops = prof["valu_insts_per_launch"] * 64.0
             roof["valu"] = {"achieved_lane_ops_per_s": lane_ops / (kern_max * 1e-3),
@@ -371,6 +484,8 @@ def main(argv=None):
             "metric": metric, "value": value, "unit": "agent-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall_max / args.steps * 1e3,
             "ms_per_step_eager": eager_max / args.steps * 1e3, "step_timing": timing,
+            "device_warmup": {"ms": round(warm_ms, 1), "steps": warm_steps,
+                              "note": "untimed replays after the W warm-up steps, before the timed region"},
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (device-RNG episodes, uniform(-1,1) actions)",
             "config": {"workload": f"N={n} drones x E={e} envs per GPU, kinematic dynamics + "
@@ -379,7 +494,9 @@ def main(argv=None):
                                    f"{', CTDE global_state emitted' if args.ctde else ''}",
                        "baseline_config": args.label,
                        "num_drones": n, "envs_per_gpu": e, "global_envs": world * e,
-                       "obs_dim": vec.obs_dim, "parallelism": f"env-sharded x{world}",
+                       "obs_dim": vec.obs_dim,
+                       "parallelism": f"env-sharded x{world}" + (f", {G} env groups per GPU on {G} HIP streams"
+                                                                  if G > 1 else ""),
                        "ctde_allgather": bool(gather_buf is not None),
                        "ctde_gather_every": args.gather_every if gather_buf is not None else None},
             "roofline": roof,

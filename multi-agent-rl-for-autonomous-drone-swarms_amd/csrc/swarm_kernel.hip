@@ -1114,8 +1114,8 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
 // so that every wave of the 8192-env headline launch is resident at once:
 //  * env-uniform data (goal, step counter, episode, base addresses) lives in SGPRs and per-lane
 //    addresses are 32-bit offsets from them (no per-lane 64-bit address arithmetic);
-//  * a 96-entry position ring (drone j at j, and at j + 64 for j < 32): rotation r reads
-//    ring[t + r] as base + immediate;
+//  * a 96-entry structure-of-arrays position ring (drone j at j, and at j + 64 for j < 32):
+//    rotation r reads soa[t + r] as base + immediate, two rotations per ds_read2_b32;
 //  * the observation row is built in registers once, staged in LDS CH rows at a time and stored
 //    with coalesced 16-B global stores.
 constexpr int S64_N = 64;
@@ -1149,15 +1149,117 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// A wave's LDS: ring + obstacles during the step, the obs staging chunk afterwards.
+// A wave's LDS: positions + obstacles during the step, the obs staging chunk afterwards.
+// Positions are held twice: `ring` (float4 per drone, for the exact finish and the obs row) and
+// the pair-pass ring as structure-of-arrays `soa` (x, y, z, eligibility planes of S64_SOA
+// floats; drone j at j and at j + 64 for j < 32), so that rotations r and r-1 of one coordinate
+// are one ds_read2_b32 into a register pair, the operand of the packed-f32 distance math.
+constexpr int S64_SOA = S64_RING;
 template <int CH>
 union S64Lds {
   struct {
-    float4 ring[S64_RING];
+    float4 ring[S64_N];
+    float soa[4 * S64_SOA];
     float4 obst[S64_MMAX];
   } w;
   float4 stage[CH * S64_D / 4];
 };
+
+// step64's pair pass: pair_pass_w64's rotation scheme (same keys, formation terms, mirror
+// exchange and results, bit for bit) with the squared distances of two rotations per packed
+// f32 operation: 3 v_pk_add + v_pk_mul + 2 v_pk_fma per two pairs instead of 12 VALU.  The
+// arithmetic per element is sqsum_rank's (fma(z,z, fma(y,y, x*x)) of the same differences).
+typedef float s64_f2 __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(3))) float s64_lds_cf;
+template <int KS, int PASS, bool FAST, int RT, int NB, bool MIRROR>
+__device__ __forceinline__ void pair_group_s64(s64_lds_cf* __restrict__ s0, uint32_t t4, float px, float py, float pz,
+                                               bool self, uint32_t sflag, uint32_t keep, uint32_t keep_m, float ds,
+                                               uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum,
+                                               float& macc) {
+  float sq[NB], term[NB];
+  bool el[NB];
+  uint32_t v[NB];
+#pragma unroll
+  for (int i = 0; i + 1 < NB; i += 2) {
+    const s64_f2 X = {s0[RT - i], s0[RT - i - 1]};
+    const s64_f2 Y = {s0[S64_SOA + RT - i], s0[S64_SOA + RT - i - 1]};
+    const s64_f2 Z = {s0[2 * S64_SOA + RT - i], s0[2 * S64_SOA + RT - i - 1]};
+    const s64_f2 dx = X - px, dy = Y - py, dz = Z - pz;
+    s64_f2 s = dx * dx;
+    s = __builtin_elementwise_fma(dy, dy, s);
+    s = __builtin_elementwise_fma(dz, dz, s);
+    sq[i] = s.x;
+    sq[i + 1] = s.y;
+  }
+  if constexpr (NB % 2) {
+    constexpr int i = NB - 1;
+    sq[i] = sqsum_rank(s0[RT - i] - px, s0[S64_SOA + RT - i] - py, s0[2 * S64_SOA + RT - i] - pz);
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) el[i] = FAST ? true : (self & (s0[3 * S64_SOA + RT - i] != 0.f));
+  float esum = 0.f;
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+    v[i] = own_pair<KS, PASS, FAST>(nk, sq[i], (uint32_t)(RT - i), el[i], keep, ds, smin, esum, term[i]);
+  if constexpr (MIRROR) {
+    uint32_t rc[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      rc[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t4 + (uint32_t)(256 - 4 * (RT - i))), (int)(v[i] | sflag));
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      mirror_pair<KS, PASS, FAST, false>(nk, rc[i], (uint32_t)(64 - RT + i), self, keep_m, ds, smin, esum);
+    if constexpr (PASS == 1) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) macc = wave_ror1(macc) + term[i];
+    }
+  }
+  if constexpr (PASS == 1) fsum += (double)esum;
+}
+template <int KS, int PASS, bool FAST, int RT, int B>
+__device__ __forceinline__ void pair_groups_s64(s64_lds_cf* __restrict__ s0, uint32_t t4, float px, float py, float pz,
+                                                bool self, uint32_t sflag, uint32_t keep, uint32_t keep_m, float ds,
+                                                uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum,
+                                                float& macc) {
+  if constexpr (RT >= 1) {
+    constexpr int NB = RT < B ? RT : B;
+    pair_group_s64<KS, PASS, FAST, RT, NB, true>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum,
+                                                 macc);
+    pair_groups_s64<KS, PASS, FAST, RT - NB, B>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum,
+                                                macc);
+  }
+}
+// `soa` = the wave's pair-pass ring (S64Lds::soa); lane t reads from soa + t.
+template <int KS, int PASS, bool FAST>
+__device__ __forceinline__ void pair_pass_s64(const float* __restrict__ soa, int t, float px, float py, float pz,
+                                              bool self, uint32_t keep, float ds, uint32_t (&nk)[KS > 0 ? KS : 1],
+                                              float& smin, double& fsum) {
+  const uint32_t sflag = (FAST || self) ? 0u : 0x80000000u;
+  const uint32_t keep_m = keep & 0x7fffffffu;
+  const uint32_t t4 = (uint32_t)t << 2;
+  // lane base &soa[t] as an opaque LDS address: every plane/rotation is then an immediate
+  // offset of ds_read2_b32 (x, y, z planes within its 1020-B reach); derived from the wave's LDS
+  // base, the compiler folds the plane offsets into one v_add per read instead
+  s64_lds_cf* s0 = (s64_lds_cf*)(soa + t);
+  asm volatile("" : "+v"(s0));
+  float macc = 0.f;
+  pair_groups_s64<KS, PASS, FAST, 31, SWARM_PAIR_BATCH>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk,
+                                                        smin, fsum, macc);
+  if constexpr (PASS == 1) fsum += (double)wave_ror1(macc);
+  // rotation 32 pairs t with t+32 from both sides: own evaluation only
+  pair_group_s64<KS, PASS, FAST, 32, 1, false>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum,
+                                               macc);
+}
+// Drone t's entry of both rings (float4 ring for the finish / obs row, SoA pair-pass ring).
+__device__ __forceinline__ void s64_put(float4* __restrict__ ring, float* __restrict__ soa, int t, float px, float py,
+                                        float pz, float w) {
+  ring[t] = make_float4(px, py, pz, w);
+  soa[t] = px; soa[S64_SOA + t] = py; soa[2 * S64_SOA + t] = pz; soa[3 * S64_SOA + t] = w;
+  if (t < S64_SOA - S64_N) {
+    soa[t + S64_N] = px; soa[S64_SOA + t + S64_N] = py; soa[2 * S64_SOA + t + S64_N] = pz;
+    soa[3 * S64_SOA + t + S64_N] = w;
+  }
+}
 
 // One env's inputs, loaded one env ahead of its compute (software pipeline): raw loaded values
 // only — any arithmetic on them here would make the wave wait for the loads right away.
@@ -1231,6 +1333,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   asm volatile("" : "+v"(t));
   const unsigned t3 = 3u * (unsigned)t;
   const size_t ea = (size_t)env * S64_N;  // first agent of the env (uniform)
+  float* __restrict__ const soa = reinterpret_cast<float*>(ring + S64_N);  // S64Lds::w.soa
   S64ArgPtr A = s64_args();  // re-fetched at every phase boundary
   STAMP_AT(env, 0);
 #ifdef SWARM_STAMPS
@@ -1281,11 +1384,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     py = clampf(py, A->P.neg_half_w, A->P.half_w);
     pz = clampf(pz, A->P.neg_half_w, A->P.half_w);
   }
-  {
-    const float4 me = make_float4(px, py, pz, act ? 1.f : 0.f);
-    ring[t] = me;
-    if (t < S64_RING - S64_N) ring[t + S64_N] = me;
-  }
+  s64_put(ring, soa, t, px, py, pz, act ? 1.f : 0.f);
   wave_sync();
   prefetch();  // `c` is dead from here on
   if constexpr (SWARM_PRIO_MODE >= 2) __builtin_amdgcn_s_setprio(1);
@@ -1313,11 +1412,11 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   }
 #endif
 #if SWARM_DIAG_NO_FORMATION
-  if (fast) pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
+  if (fast) pair_pass_s64<KS, 0, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
 #else
-  if (fast) pair_pass_w64<KS, 1, true>(ring, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
+  if (fast) pair_pass_s64<KS, 1, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
 #endif
-  else pair_pass_w64<KS, 1, false>(ring, t, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
+  else pair_pass_s64<KS, 1, false>(soa, t, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
   obstacle_pass<MSL, true>(obst, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
   if constexpr (LANDED) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next env's inputs are in
   STAMP_AT(env, 3);
@@ -1334,14 +1433,20 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     if (slow_nb) exact_select<KS, false>(ring, S64_N, t, S64_K, max_first(wd, S64_K), px, py, pz, wd, wj);
     if (slow_ob) exact_select<MSL, true>(obst, M, -1, S64_MS, max_first(od, S64_MS), px, py, pz, od, oj);
   };
-  select_topk(true);
   STAMP_AT(env, 4);
-  A = s64_args();
 
   // ---- rewards / terminations: drone_swarm_env.py:120-172
+  // The pair collision comes from the nearest key, not from the exact top-K: the finish runs
+  // only for the observation that is emitted (after the reset decision), so a resetting env
+  // pays one finish, not two.  Fast path: the nearest key bounds the exact nearest distance,
+  // [key & keep, key | ~keep] x [FAST_LO, FAST_HI] (truncated d~ within 2^-21 of exact); only
+  // a nearest distance inside that band (~1e-5 of the threshold) needs the exact scan.
   bool pcoll;
   if (fast) {
-    pcoll = wd[0] <= A->P.thr_pair;
+    const uint32_t keep = A->P.nb_keep;
+    pcoll = __uint_as_float(nk[0] | ~keep) * FAST_HI <= A->P.thr_pair;
+    if (!pcoll && __uint_as_float(nk[0] & keep) * FAST_LO <= A->P.thr_pair)
+      pcoll = exact_pair_collision(ring, S64_N, t, px, py, pz, A->P.s_pair);
   } else {
     pcoll = smin <= A->P.thr_pair * FAST_LO;
     if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act)
@@ -1414,9 +1519,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     gx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ox), M));
     gy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(oy), M));
     gz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(oz), M));
-    const float4 me = make_float4(px, py, pz, 1.f);
-    ring[t] = me;
-    if (t < S64_RING - S64_N) ring[t + S64_N] = me;
+    s64_put(ring, soa, t, px, py, pz, 1.f);
     wave_sync();
 #pragma unroll
     for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
@@ -1425,9 +1528,11 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     bool c2 = false;
     float s2 = 0.f;
     double f2 = 0.0;
-    pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, A->P.nb_keep, 0.f, nk, s2, f2);
+    pair_pass_s64<KS, 0, true>(soa, t, px, py, pz, true, A->P.nb_keep, 0.f, nk, s2, f2);
     obstacle_pass<MSL, false>(obst, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
     select_topk(false);
+  } else {
+    select_topk(true);
   }
 
   STAMP_AT(env, 6);

@@ -12,6 +12,14 @@ re-drawn in the same launch (Philox stream keyed by seed, global env index and e
 `obs` then holds the new episode's first observation — the reference emits no terminal obs
 (drone_swarm_env.py:154), so nothing is lost.  env_done carries terminated/truncated["__all__"]
 and a RESET bit.
+
+Env groups (`groups=G`): the E envs are split into G contiguous blocks, each stepped by its own
+launch on its own HIP stream (`group_streams`).  Envs are independent, so a group's step k+1
+needs only that group's step k: with `step(..., join=False)` (or `step_group` on the group
+streams) the launches of different groups overlap, and one group's load burst and completion
+tail run under another group's steady state instead of idling the CUs.  Every env is still
+stepped exactly once per step; results are bitwise those of G = 1 (the reset RNG is keyed by the
+global env index).
 """
 from __future__ import annotations
 
@@ -38,7 +46,8 @@ class VecSwarm:
                  auto_reset: bool = True, seed: int = 0, env_offset: int = 0,
                  device: str | torch.device | None = None, with_infos: bool = False,
                  with_global_state: bool = False, physics: dict[str, Any] | None = None,
-                 kernel_path: str = "auto", persistent: bool = True, waves_per_simd: int = 0):
+                 kernel_path: str = "auto", persistent: bool = True, waves_per_simd: int = 0,
+                 groups: int = 1):
         if isinstance(config, DroneEnvConfig):
             cfg, raw = config, {}
         else:
@@ -96,6 +105,28 @@ class VecSwarm:
         nat.check(self.lib.swarm_query_launch(ctypes.byref(p), ctypes.byref(self.launch_info)),
                   self.lib)
         self.obs_dim = int(self.lib.swarm_obs_dim(ctypes.byref(p)))
+        # ---- env groups: contiguous env blocks, one launch (and stream) each
+        g_n = int(groups)
+        if not 1 <= g_n <= max(1, self.num_envs):
+            raise ValueError(f"groups must be in [1, num_envs], got {groups}")
+        self.groups = g_n
+        q, r = divmod(self.num_envs, g_n)
+        bounds = [0]
+        for g in range(g_n):
+            bounds.append(bounds[-1] + q + (1 if g < r else 0))
+        self.group_slices = [(bounds[g], bounds[g + 1]) for g in range(g_n)]
+        self._gparams, self.group_launch_info = [], []
+        for lo, hi in self.group_slices:
+            pg = nat.SwarmParams()
+            ctypes.memmove(ctypes.byref(pg), ctypes.byref(p), ctypes.sizeof(p))
+            pg.num_envs = hi - lo
+            pg.env_offset = int(env_offset) + lo
+            li = nat.SwarmLaunchInfo()
+            nat.check(self.lib.swarm_query_launch(ctypes.byref(pg), ctypes.byref(li)), self.lib)
+            self._gparams.append(pg)
+            self.group_launch_info.append(li)
+        self.group_streams = ([torch.cuda.Stream(self.device) for _ in range(g_n)]
+                              if g_n > 1 else None)
 
         e, m, d = self.num_envs, int(cfg.num_obstacles), self.obs_dim
         kw = dict(device=self.device)
@@ -109,8 +140,9 @@ class VecSwarm:
         self.step_count = torch.zeros((e,), dtype=torch.int32, **kw)
         self.episode = torch.zeros((e,), dtype=torch.int32, **kw)  # read as uint32 by the kernel
         self.damping = torch.zeros((e, n), dtype=f32, **kw)
-        # env-queue heads of the persistent step kernel (zero, and left zero by every launch)
-        self.work = (torch.zeros((nat.WORK_WORDS,), dtype=torch.int32, **kw)
+        # env-queue heads of the persistent step kernel, one row per group (zero, and left
+        # zero by every launch)
+        self.work = (torch.zeros((self.groups, nat.WORK_WORDS), dtype=torch.int32, **kw)
                      if self.persistent else None)
         # ---- outputs (persistent buffers)
         self.obs = torch.zeros((e, n, d), dtype=f32, **kw)
@@ -126,19 +158,27 @@ class VecSwarm:
 
     # ------------------------------------------------------------------ plumbing
     def _bind(self) -> None:
-        s = nat.SwarmState()
-        s.pos, s.vel, s.goal = _ptr(self.pos), _ptr(self.vel), _ptr(self.goal)
-        s.obstacles = _ptr(self.obstacles) if self.obstacles.numel() else None
-        s.active, s.step_count = _ptr(self.active), _ptr(self.step_count)
-        s.episode, s.damping = _ptr(self.episode), _ptr(self.damping)
-        s.work = _ptr(self.work)
-        o = nat.SwarmOut()
-        o.obs, o.reward = _ptr(self.obs), _ptr(self.reward)
-        o.terminated, o.truncated = _ptr(self.terminated), _ptr(self.truncated)
-        o.env_done = _ptr(self.env_done)
-        o.dist_goal, o.info_flags = _ptr(self.dist_goal), _ptr(self.info_flags)
-        o.global_state = _ptr(self.global_state)
-        self._state_c, self._out_c = s, o
+        """ctypes state/out blocks per group: row `lo` of every [E, ...] tensor onwards."""
+        def off(t, lo):
+            return None if t is None else t.data_ptr() + lo * t.stride(0) * t.element_size()
+
+        self._gstate, self._gout = [], []
+        for g, (lo, _) in enumerate(self.group_slices):
+            s = nat.SwarmState()
+            s.pos, s.vel, s.goal = off(self.pos, lo), off(self.vel, lo), off(self.goal, lo)
+            s.obstacles = off(self.obstacles, lo) if self.obstacles.numel() else None
+            s.active, s.step_count = off(self.active, lo), off(self.step_count, lo)
+            s.episode, s.damping = off(self.episode, lo), off(self.damping, lo)
+            s.work = None if self.work is None else _ptr(self.work[g])
+            o = nat.SwarmOut()
+            o.obs, o.reward = off(self.obs, lo), off(self.reward, lo)
+            o.terminated, o.truncated = off(self.terminated, lo), off(self.truncated, lo)
+            o.env_done = off(self.env_done, lo)
+            o.dist_goal, o.info_flags = off(self.dist_goal, lo), off(self.info_flags, lo)
+            o.global_state = off(self.global_state, lo)
+            self._gstate.append(s)
+            self._gout.append(o)
+        self._state_c, self._out_c = self._gstate[0], self._gout[0]
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -166,44 +206,92 @@ class VecSwarm:
         return mk.data_ptr()
 
     # ------------------------------------------------------------------ API
-    def step(self, actions: torch.Tensor, action_mask: torch.Tensor | None = None):
-        """One step of all envs.  actions [E,N,3] float32 on the device.
-
-        Returns (obs [E,N,D], reward [E,N] f32, terminated [E,N] bool, truncated [E,N] bool,
-        env_done [E] u8 bits).  Views into persistent buffers.
-        """
+    def _actions(self, actions, action_mask):
         self._check_tensor("actions", actions, (self.num_envs, self.num_drones, 3), torch.float32)
-        am = None
         if action_mask is not None:
             if action_mask.dtype == torch.bool:
                 action_mask = action_mask.view(torch.uint8)
             self._check_tensor("action_mask", action_mask, (self.num_envs, self.num_drones),
                                torch.uint8)
-            am = action_mask.data_ptr()
-        rc = self.lib.swarm_step(ctypes.byref(self.params), ctypes.byref(self._state_c),
-                                 actions.data_ptr(), am, ctypes.byref(self._out_c), self._stream())
+        return actions, action_mask
+
+    def _launch_step(self, g: int, actions, action_mask, stream: int) -> None:
+        lo = self.group_slices[g][0]
+        a = actions.data_ptr() + lo * actions.stride(0) * actions.element_size()
+        am = None if action_mask is None else action_mask.data_ptr() + lo * action_mask.stride(0)
+        rc = self.lib.swarm_step(ctypes.byref(self._gparams[g]), ctypes.byref(self._gstate[g]), a, am,
+                                 ctypes.byref(self._gout[g]), stream)
         nat.check(rc, self.lib)
+
+    def step(self, actions: torch.Tensor, action_mask: torch.Tensor | None = None, *,
+             join: bool = True):
+        """One step of all envs.  actions [E,N,3] float32 on the device.
+
+        Returns (obs [E,N,D], reward [E,N] f32, terminated [E,N] bool, truncated [E,N] bool,
+        env_done [E] u8 bits).  Views into persistent buffers.
+
+        With env groups the launches fork from the current stream onto the group streams; with
+        join=False they are not joined back (call `join()` before using the outputs on another
+        stream), so consecutive steps of different groups overlap.
+        """
+        actions, action_mask = self._actions(actions, action_mask)
+        if self.groups == 1:
+            self._launch_step(0, actions, action_mask, self._stream())
+            return self.obs, self.reward, self.terminated, self.truncated, self.env_done
+        cur = torch.cuda.current_stream(self.device)
+        fork = torch.cuda.Event()
+        fork.record(cur)
+        for g, st in enumerate(self.group_streams):
+            st.wait_event(fork)
+            self._launch_step(g, actions, action_mask, st.cuda_stream)
+            if not join:  # the caller's tensors are in use on the group stream
+                actions.record_stream(st)
+                if action_mask is not None:
+                    action_mask.record_stream(st)
+        if join:
+            self.join()
         return self.obs, self.reward, self.terminated, self.truncated, self.env_done
+
+    def step_group(self, g: int, actions: torch.Tensor, action_mask: torch.Tensor | None = None):
+        """Step env group `g` only (rows group_slices[g] of the full-batch tensors) on the
+        current stream — e.g. inside `torch.cuda.stream(vec.group_streams[g])` or a hipGraph
+        capture on that stream.  actions is the full [E,N,3] tensor."""
+        if not 0 <= g < self.groups:
+            raise ValueError(f"group {g} out of range [0, {self.groups})")
+        actions, action_mask = self._actions(actions, action_mask)
+        self._launch_step(g, actions, action_mask, self._stream())
+        return self.obs, self.reward, self.terminated, self.truncated, self.env_done
+
+    def join(self) -> None:
+        """Make the current stream wait for every group stream."""
+        if self.group_streams is None:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        for st in self.group_streams:
+            cur.wait_stream(st)
+
+    def _aux(self, fn, env_mask) -> None:
+        self.join()
+        mp = self._mask_ptr(env_mask)
+        for g, (lo, _) in enumerate(self.group_slices):
+            rc = fn(ctypes.byref(self._gparams[g]), ctypes.byref(self._gstate[g]),
+                    None if mp is None else mp + lo, ctypes.byref(self._gout[g]), self._stream())
+            nat.check(rc, self.lib)
 
     def reset(self, env_mask: torch.Tensor | None = None) -> torch.Tensor:
         """Device reset (Philox draws) of the masked envs (all if None); returns obs."""
-        rc = self.lib.swarm_reset(ctypes.byref(self.params), ctypes.byref(self._state_c),
-                                  self._mask_ptr(env_mask), ctypes.byref(self._out_c),
-                                  self._stream())
-        nat.check(rc, self.lib)
+        self._aux(self.lib.swarm_reset, env_mask)
         return self.obs
 
     def observe(self, env_mask: torch.Tensor | None = None) -> torch.Tensor:
         """obs / dist_goal / global_state of the current state (no state change)."""
-        rc = self.lib.swarm_observe(ctypes.byref(self.params), ctypes.byref(self._state_c),
-                                    self._mask_ptr(env_mask), ctypes.byref(self._out_c),
-                                    self._stream())
-        nat.check(rc, self.lib)
+        self._aux(self.lib.swarm_observe, env_mask)
         return self.obs
 
     def set_state(self, *, pos=None, vel=None, goal=None, obstacles=None, active=None,
                   step_count=None, episode=None, damping=None) -> None:
         """Inject state (host or device arrays); shapes as the state tensors."""
+        self.join()
         for name, val in (("pos", pos), ("vel", vel), ("goal", goal), ("obstacles", obstacles),
                           ("active", active), ("step_count", step_count),
                           ("episode", episode), ("damping", damping)):
@@ -230,8 +318,9 @@ class VecSwarm:
         """Kernel the step launches: the headline specialisation swarm_step64_once<32, 4> (one
         wave per env, 4 per workgroup) or its persistent form swarm_step64<32> (E larger than
         the resident grid, env queues in `work`), else the generic swarm_kernel<KIND, DYN, KS,
-        MSL, LM> (KIND 0 = step; LM lane mode 0 block / 1 multi-team wave / 2 one team per wave)."""
-        li = self.launch_info
+        MSL, LM> (KIND 0 = step; LM lane mode 0 block / 1 multi-team wave / 2 one team per wave).
+        With env groups: the kernel of group 0."""
+        li = self.group_launch_info[0]
         kid = int(li.kernel_id)
         if kid == nat.KERNEL_STEP64_PERSISTENT and self.persistent:
             return "swarm_step64<32>"

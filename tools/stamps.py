@@ -19,6 +19,7 @@ if sys.argv[1] == "build":
                     "-fno-slp-vectorize", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
                     "-I", str(ROOT / "include"), "-DSWARM_STAMPS", "-DSWARM_DEV_HOT", *sys.argv[2:],
                     str(ROOT / "multi-agent-rl-for-autonomous-drone-swarms_amd/csrc/swarm_kernel.hip"),
+                    str(ROOT / "multi-agent-rl-for-autonomous-drone-swarms_amd/csrc/swarm_policy.hip"),
                     "-o", str(LIB)], check=True)
     sys.exit(0)
 
