@@ -348,7 +348,11 @@ def main(argv=None):
                 out.append(gr)
             return out
         graphs = capture(args.ring)
-        tail = capture(rem) if rem else None  # the K % ring remainder, also replayed from a graph
+        # short timed regions (the driver's K = 20) replay all K steps from one graph per group,
+        # so that the wall clock holds one graph launch per group; longer ones replay ring
+        # segments plus a graph of the K % ring remainder
+        whole = capture(args.steps) if args.steps <= 256 else None
+        tail = capture(rem) if rem and whole is None else None
 
         def replay_all(gs):
             if G == 1:
@@ -363,13 +367,17 @@ def main(argv=None):
         def body():
             t_ev[0].record(stream)
             fork(t_ev[0])
-            for _ in range(reps):
-                replay_all(graphs)
-            if tail is not None:
-                replay_all(tail)
+            if whole is not None:
+                replay_all(whole)
+            else:
+                for _ in range(reps):
+                    replay_all(graphs)
+                if tail is not None:
+                    replay_all(tail)
             join()
             t_ev[1].record(stream)
-        timing = f"hipGraph replay of {args.ring}-step segments" + (
+        timing = (f"hipGraph replay of the {args.steps} steps (actions from a {args.ring}-tensor ring)"
+                  if whole is not None else f"hipGraph replay of {args.ring}-step segments") + (
             f", {G} env groups on {G} HIP streams (one graph per group)" if G > 1 else "") + (
             f" (policy {args.policy} + env step per step)" if pol is not None else "")
     else:

@@ -1161,6 +1161,7 @@ union S64Lds {
     float4 ring[S64_N];
     float soa[4 * S64_SOA];
     float4 obst[S64_MMAX];
+    float osoa[3 * S64_MMAX];  // obstacle x, y, z planes (packed-f32 obstacle pass)
   } w;
   float4 stage[CH * S64_D / 4];
 };
@@ -1198,9 +1199,31 @@ __device__ __forceinline__ void pair_group_s64(s64_lds_cf* __restrict__ s0, uint
 #pragma unroll
   for (int i = 0; i < NB; ++i) el[i] = FAST ? true : (self & (s0[3 * S64_SOA + RT - i] != 0.f));
   float esum = 0.f;
+  if constexpr (PASS == 1 && FAST) {
+    // own_pair's FAST kinematic body with the formation differences d~ - d* of two rotations
+    // in one v_pk_add_f32 (same values, same summation order)
+    float dv[NB];
 #pragma unroll
-  for (int i = 0; i < NB; ++i)
-    v[i] = own_pair<KS, PASS, FAST>(nk, sq[i], (uint32_t)(RT - i), el[i], keep, ds, smin, esum, term[i]);
+    for (int i = 0; i < NB; ++i) dv[i] = pair_value<PASS>(sq[i]);
+#pragma unroll
+    for (int i = 0; i + 1 < NB; i += 2) {
+      const s64_f2 V = {dv[i], dv[i + 1]};
+      const s64_f2 Ed = V - ds;
+      term[i] = fabsf(Ed.x);
+      term[i + 1] = fabsf(Ed.y);
+    }
+    if constexpr (NB % 2) term[NB - 1] = fabsf(dv[NB - 1] - ds);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      if constexpr (KS > 0) kins<KS>(nk, (__float_as_uint(dv[i]) & keep) | (uint32_t)(RT - i));
+      esum += term[i];
+      v[i] = __float_as_uint(dv[i]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      v[i] = own_pair<KS, PASS, FAST>(nk, sq[i], (uint32_t)(RT - i), el[i], keep, ds, smin, esum, term[i]);
+  }
   if constexpr (MIRROR) {
     uint32_t rc[NB];
 #pragma unroll
@@ -1250,6 +1273,38 @@ __device__ __forceinline__ void pair_pass_s64(const float* __restrict__ soa, int
   pair_group_s64<KS, PASS, FAST, 32, 1, false>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum,
                                                macc);
 }
+// step64's obstacle pass: obstacle_pass's exact axis-path squared sums ((x*x + y*y) + z*z, no
+// FMA) and keys for two obstacles per packed-f32 operation, from the obstacle planes `os`
+// (x at os[m], y at os[16 + m], z at os[32 + m]; all lanes read the same word: LDS broadcast).
+template <int MSL, bool COLL>
+__device__ __forceinline__ void obstacle_pass_s64(const float* __restrict__ os, int M, float px, float py, float pz,
+                                                  bool chk, float s_thr, uint32_t keep,
+                                                  uint32_t (&ok)[MSL > 0 ? MSL : 1], bool& coll) {
+  int m = 0;
+  for (; m + 1 < M; m += 2) {
+    const s64_f2 X = {os[m], os[m + 1]};
+    const s64_f2 Y = {os[S64_MMAX + m], os[S64_MMAX + m + 1]};
+    const s64_f2 Z = {os[2 * S64_MMAX + m], os[2 * S64_MMAX + m + 1]};
+    const s64_f2 dx = X - px, dy = Y - py, dz = Z - pz;
+    const s64_f2 sq = (dx * dx + dy * dy) + dz * dz;
+    if constexpr (MSL > 0) {
+      kins<MSL>(ok, (__float_as_uint(sq.x) & keep) | (uint32_t)m);
+      kins<MSL>(ok, (__float_as_uint(sq.y) & keep) | (uint32_t)(m + 1));
+    }
+    if constexpr (COLL) coll = coll || (chk && ((sq.x <= s_thr) || (sq.y <= s_thr)));
+  }
+  if (m < M) {
+    const float sq = sqsum_f(os[m] - px, os[S64_MMAX + m] - py, os[2 * S64_MMAX + m] - pz);
+    if constexpr (MSL > 0) kins<MSL>(ok, (__float_as_uint(sq) & keep) | (uint32_t)m);
+    if constexpr (COLL) coll = coll || (chk && (sq <= s_thr));
+  }
+}
+__device__ __forceinline__ void s64_put_obst(float4* __restrict__ obst, float* __restrict__ os, int t, float ox,
+                                             float oy, float oz) {
+  obst[t] = make_float4(ox, oy, oz, 0.f);
+  os[t] = ox; os[S64_MMAX + t] = oy; os[2 * S64_MMAX + t] = oz;
+}
+
 // Drone t's entry of both rings (float4 ring for the finish / obs row, SoA pair-pass ring).
 __device__ __forceinline__ void s64_put(float4* __restrict__ ring, float* __restrict__ soa, int t, float px, float py,
                                         float pz, float w) {
@@ -1351,7 +1406,8 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   float px = c.px, py = c.py, pz = c.pz;
   float vx = c.vx, vy = c.vy, vz = c.vz;
   bool act = c.act != 0;
-  if (t < M) obst[t] = make_float4(c.ox, c.oy, c.oz, 0.f);
+  float* __restrict__ const osoa = reinterpret_cast<float*>(obst + S64_MMAX);  // S64Lds::w.osoa
+  if (t < M) s64_put_obst(obst, osoa, t, c.ox, c.oy, c.oz);
   const int n_active = __popcll(__ballot(act));
   STAMP_AT(env, 1);
 
@@ -1417,7 +1473,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   if (fast) pair_pass_s64<KS, 1, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
 #endif
   else pair_pass_s64<KS, 1, false>(soa, t, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
-  obstacle_pass<MSL, true>(obst, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
+  obstacle_pass_s64<MSL, true>(osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
   if constexpr (LANDED) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next env's inputs are in
   STAMP_AT(env, 3);
   A = s64_args();
@@ -1515,7 +1571,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     act = true;
     const float ox = uni(wo[0], lo_w, wd_w), oy = uni(wo[1], lo_w, wd_w), oz = uni(wo[2], lo_w, wd_w);
     wave_sync();  // every read of the old ring / obstacles is done
-    if (t < M) obst[t] = make_float4(ox, oy, oz, 0.f);
+    if (t < M) s64_put_obst(obst, osoa, t, ox, oy, oz);
     gx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ox), M));
     gy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(oy), M));
     gz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(oz), M));
@@ -1529,7 +1585,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     float s2 = 0.f;
     double f2 = 0.0;
     pair_pass_s64<KS, 0, true>(soa, t, px, py, pz, true, A->P.nb_keep, 0.f, nk, s2, f2);
-    obstacle_pass<MSL, false>(obst, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
+    obstacle_pass_s64<MSL, false>(osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
     select_topk(false);
   } else {
     select_topk(true);
