@@ -52,7 +52,7 @@ PRESETS = {
                      label="config 3: N=64 x E=8192 on 1 MI355X (headline); config 4 per GPU"),
     "n16": dict(drones=16, envs=1024, ctde=False,
                 label="config 2: N=16 x E=1024 on 1 MI355X (launch-latency-bound)"),
-    "n256": dict(drones=256, envs=1024, ctde=True,
+    "n256": dict(drones=256, envs=1024, ctde=True, groups=2,
                  label="config 5 per-GPU slab: N=256 x E=1024 with CTDE global_state"),
 }
 
@@ -89,7 +89,8 @@ def parse(argv=None):
                          "warm-up steps (GPU clocks ramp over ~100 ms; reported in the JSON line)")
     ap.add_argument("--groups", type=int, default=None,
                     help="env groups per GPU, each stepped on its own HIP stream (VecSwarm groups=G); "
-                         "default 2 for the headline, 1 otherwise")
+                         "default 2 for the headline and n256 (1 for n256 with a multi-rank CTDE "
+                         "gather), 1 for n16")
     ap.add_argument("--gather-every", type=int, default=8,
                     help="CTDE all-gather period in steps (SURVEY.md §5: per batch, not per step)")
     a = ap.parse_args(argv)
@@ -98,12 +99,12 @@ def parse(argv=None):
     a.envs = pre["envs"] if a.envs is None else a.envs
     a.ctde = pre["ctde"] if a.ctde is None else a.ctde
     a.label = pre["label"]
+    a.groups_explicit = a.groups is not None
     if a.groups is None:
         a.groups = pre.get("groups", 1)
     if a.groups < 1:
         ap.error("--groups must be >= 1")
-    if a.ctde and a.groups > 1:
-        ap.error("--ctde gathers the whole batch's global_state: use --groups 1")
+
     if a.gather_every < 1:
         ap.error("--gather-every must be >= 1")
     return a
@@ -251,6 +252,10 @@ def main(argv=None):
 
     n = args.drones
     offset, e = shard_plan(world, rank, args.envs)
+    if args.ctde and world > 1 and args.groups > 1:  # the gather reads the whole batch each period
+        if args.groups_explicit:
+            raise SystemExit("--ctde with several ranks gathers the whole batch's global_state: use --groups 1")
+        args.groups = 1
     raw = {"num_drones": n}
     if args.no_term:
         raw.update(collision_radius=0.0, obstacle_radius=0.0, goal_radius=0.0)
