@@ -19,7 +19,7 @@ import torch
 from .. import _native as nat
 from ..vec_env import VecSwarm
 from .common import Box, DroneEnvConfig, MultiAgentEnv
-from .drone_swarm_env import _host
+from .drone_swarm_env import PackedIO, _host
 from .host_reset import physics_reset_draws
 
 
@@ -42,7 +42,8 @@ class DronePhysicsEnv(MultiAgentEnv):
         self.masses = np.ones(self.num_drones, np.float32)
         self._vec = VecSwarm(1, self.cfg, num_drones=self.num_drones, dynamics="physics",
                              auto_reset=False, with_infos=True, with_global_state=True,
-                             physics=physics)
+                             physics=physics, packed_io=True)
+        self._io = PackedIO(self._vec)
 
     @property
     def goal(self) -> np.ndarray:
@@ -77,8 +78,8 @@ class DronePhysicsEnv(MultiAgentEnv):
                             obstacles=obst[None], active=np.ones((1, n), bool),
                             step_count=np.zeros(1, np.int32), damping=damping[None])
         self._vec.observe()
-        obs = _host(self._vec.obs[0])
-        dist = _host(self._vec.dist_goal[0])
+        h = self._io.fetch()
+        obs, dist = h["obs"][0], h["dist_goal"][0]
         observations = {a: obs[i].copy() for i, a in enumerate(self.agent_ids)}
         infos = {a: {"distance_to_goal": float(dist[i]), "reached_goal": False, "collision": False}
                  for i, a in enumerate(self.agent_ids)}
@@ -89,26 +90,24 @@ class DronePhysicsEnv(MultiAgentEnv):
         self.goal = np.asarray(new_pos, np.float32)
 
     def step(self, action_dict: dict[str, Any]):
-        n = self.num_drones
-        acts = np.zeros((1, n, 3), np.float32)
-        mask = np.zeros((1, n), np.uint8)
+        io, v = self._io, self._vec
+        acts, mask, act = io.h_in["actions"][0], io.h_in["action_mask"][0], io.h_in["active"][0]
+        acts.fill(0.0)
+        mask.fill(0)
+        act.fill(False)
         for aid, a in action_dict.items():
             idx = self.agent_ids.index(aid)  # unknown id -> ValueError, as :326
-            acts[0, idx] = np.asarray(a, np.float32).reshape(3)  # no action clip (:336)
-            mask[0, idx] = 1
-        act = np.zeros((1, n), bool)
+            acts[idx] = np.asarray(a, np.float32).reshape(3)  # no action clip (:336)
+            mask[idx] = 1
         for a in self.agents:
-            act[0, self.agent_id_to_index[a]] = True
-        v = self._vec
-        v.active.copy_(torch.as_tensor(act).to(v.device))
-        v.step(torch.as_tensor(acts).to(v.device), torch.as_tensor(mask).to(v.device))
+            act[self.agent_id_to_index[a]] = True
+        io.send()
+        v.step(v.actions_in, v.action_mask_in)
         self.step_count += 1
-        obs = _host(v.obs[0])
-        rew = _host(v.reward[0])
-        dist = _host(v.dist_goal[0])
-        flags = _host(v.info_flags[0])
-        gs = _host(v.global_state[0])
-        env_done = int(v.env_done[0].item())
+        h = io.fetch()
+        obs, rew, dist, flags = h["obs"][0], h["reward"][0], h["dist_goal"][0], h["info_flags"][0]
+        gs = h["global_state"][0]
+        env_done = int(h["env_done"][0])
         observations = {a: obs[i].copy() for i, a in enumerate(self.agent_ids)}  # all agents
         rewards = {a: float(rew[self.agent_id_to_index[a]]) for a in self.agents}
         term_all = bool(env_done & nat.ENV_TERMINATED)

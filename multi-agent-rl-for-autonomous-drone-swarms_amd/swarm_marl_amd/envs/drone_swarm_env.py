@@ -6,7 +6,9 @@ Same constructor, attributes and dict API as src/swarm_marl/envs/drone_swarm_env
 so `register_env(name, lambda cfg: DroneSwarmEnv(cfg))` in the reference's train_*.py scripts
 works unchanged.  Behind the dict surface one env is a VecSwarm of E=1 on the GPU: the whole
 step (integrate, distances, collision, formation, rewards, kNN observation) is one kernel launch;
-only the dict assembly stays on the host.
+only the dict assembly stays on the host.  Per step the host fills one pinned input block
+(actions + active mask), which goes over in ONE async H2D copy; the kernel writes every output
+into one device arena, which comes back in ONE async D2H copy; one stream synchronisation.
 
 Seeded resets draw from numpy.random.default_rng exactly like the reference (host_reset.py), so
 the same seeds give the same episodes; rewards are float32-accurate (|err| < 1e-5).
@@ -46,8 +48,10 @@ class DroneSwarmEnv(MultiAgentEnv):
                                      dtype=np.float32)
         self.action_space = Box(low=-1.0, high=1.0, shape=(3,), dtype=np.float32)
         self._vec = VecSwarm(1, self.cfg, num_drones=self.num_drones, dynamics="kinematic",
-                             auto_reset=False, with_infos=True, with_global_state=True)
+                             auto_reset=False, with_infos=True, with_global_state=True,
+                             packed_io=True)
         self._vec.active.fill_(True)
+        self._io = PackedIO(self._vec)
 
     # ---- state attributes read (and written) by callers: visualize_swarm.py:76-110 ----------
     @property
@@ -90,12 +94,6 @@ class DroneSwarmEnv(MultiAgentEnv):
     def step_count(self, v: int) -> None:
         self._vec.step_count[0] = int(v)
 
-    def _sync_active(self) -> None:
-        mask = np.zeros(self.num_drones, bool)
-        for a in self.agents:
-            mask[self.agent_id_to_index[a]] = True
-        self._vec.active[0].copy_(torch.as_tensor(mask))
-
     # ---- API -------------------------------------------------------------------------------
     def reset(self, *, seed: int | None = None, options: dict[str, Any] | None = None):
         if seed is not None:
@@ -108,9 +106,8 @@ class DroneSwarmEnv(MultiAgentEnv):
                     goal=goal[None], obstacles=obst[None], active=np.ones((1, self.num_drones), bool),
                     step_count=np.zeros(1, np.int32))
         v.observe()
-        obs = _host(v.obs[0])
-        dist = _host(v.dist_goal[0])
-        gs = _host(v.global_state[0])
+        h = self._io.fetch()
+        obs, dist, gs = h["obs"][0], h["dist_goal"][0], h["global_state"][0]
         observations = {a: obs[i].copy() for i, a in enumerate(self.agent_ids)}
         infos = {a: {"distance_to_goal": float(dist[i]), "global_state": gs.copy()}
                  for i, a in enumerate(self.agent_ids)}
@@ -119,29 +116,43 @@ class DroneSwarmEnv(MultiAgentEnv):
     def step(self, action_dict: dict[str, Any]):
         if not self.agents:  # drone_swarm_env.py:93-95
             return {}, {}, {"__all__": True}, {"__all__": False}, {}
-        self._sync_active()
-        acts = np.zeros((1, self.num_drones, 3), np.float32)
+        io = self._io
+        acts, active = io.h_in["actions"][0], io.h_in["active"][0]
+        acts.fill(0.0)
+        active.fill(False)
+        idx = self.agent_id_to_index
         for a in self.agents:  # missing -> zero action, unknown ids ignored (:103-104)
+            i = idx[a]
+            active[i] = True
             if a in action_dict:
-                acts[0, self.agent_id_to_index[a]] = np.asarray(action_dict[a], np.float32).reshape(3)
-        v = self._vec
-        v.step(torch.as_tensor(acts).to(v.device))
-        return self._collect()
+                acts[i] = np.asarray(action_dict[a], np.float32).reshape(3)
+        io.send()
+        self._vec.step(self._vec.actions_in)
+        h = io.fetch()
+        return build_step_dicts(self.agent_ids, h["obs"][0], h["reward"][0], h["terminated"][0],
+                                h["truncated"][0], h["info_flags"][0], h["dist_goal"][0],
+                                h["global_state"][0], int(h["env_done"][0]), self)
 
-    def _collect(self):
-        v = self._vec
-        packed = torch.cat([v.obs[0].reshape(-1), v.reward[0], v.dist_goal[0],
-                            v.global_state[0]]).to("cpu").numpy()
-        flags = _host(torch.stack([v.terminated[0].to(torch.uint8), v.truncated[0].to(torch.uint8),
-                                   v.info_flags[0]]))
-        env_done = int(v.env_done[0].item())
-        n, d = self.num_drones, self._obs_dim
-        obs = packed[: n * d].reshape(n, d)
-        rew = packed[n * d: n * d + n]
-        dist = packed[n * d + n: n * d + 2 * n]
-        gs = packed[n * d + 2 * n:]
-        return build_step_dicts(self.agent_ids, obs, rew, flags[0], flags[1], flags[2], dist, gs,
-                                env_done, self)
+
+class PackedIO:
+    """Pinned host mirrors of a packed_io VecSwarm's input and output arenas: send() is one async
+    H2D copy of the inputs, fetch() one async D2H copy of every output plus one stream sync, and
+    returns numpy views of the host mirror (overwritten by the next fetch)."""
+
+    def __init__(self, vec: VecSwarm):
+        self.vec = vec
+        self._hin = torch.empty(vec.in_arena.shape, dtype=torch.uint8, pin_memory=True)
+        self._hout = torch.empty(vec.out_arena.shape, dtype=torch.uint8, pin_memory=True)
+        self.h_in = {k: t.numpy() for k, t in VecSwarm.arena_views(self._hin, vec.in_layout).items()}
+        self.h_out = {k: t.numpy() for k, t in VecSwarm.arena_views(self._hout, vec.out_layout).items()}
+
+    def send(self) -> None:
+        self.vec.in_arena.copy_(self._hin, non_blocking=True)
+
+    def fetch(self) -> dict[str, np.ndarray]:
+        self._hout.copy_(self.vec.out_arena, non_blocking=True)
+        torch.cuda.current_stream(self.vec.device).synchronize()
+        return self.h_out
 
 
 def build_step_dicts(agent_ids, obs, rew, term, trunc, info_flags, dist, gs, env_done, env=None):

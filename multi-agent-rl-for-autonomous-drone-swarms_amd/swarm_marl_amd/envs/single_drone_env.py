@@ -16,7 +16,7 @@ import torch
 from .. import _native as nat
 from ..vec_env import VecSwarm
 from .common import Box, DroneEnvConfig, GymEnv
-from .drone_swarm_env import _host
+from .drone_swarm_env import PackedIO, _host
 from .host_reset import swarm_reset_draws
 
 
@@ -34,7 +34,8 @@ class SingleDroneEnv(GymEnv):
         self.step_count = 0
         self._vec = VecSwarm(1, replace(self.cfg, neighbor_k=0, max_steps=2 ** 31 - 1),
                              num_drones=1, dynamics="kinematic", auto_reset=False,
-                             with_infos=True)
+                             with_infos=True, packed_io=True)
+        self._io = PackedIO(self._vec)
 
     @property
     def position(self) -> np.ndarray:
@@ -63,19 +64,21 @@ class SingleDroneEnv(GymEnv):
                             obstacles=obst[None], active=np.ones((1, 1), bool),
                             step_count=np.zeros(1, np.int32))
         self._vec.observe()
-        return _host(self._vec.obs[0, 0]).copy(), {
-            "distance_to_goal": float(_host(self._vec.dist_goal[0])[0])}
+        h = self._io.fetch()
+        return h["obs"][0, 0].copy(), {"distance_to_goal": float(h["dist_goal"][0, 0])}
 
     def step(self, action):
-        v = self._vec
-        a = np.asarray(action, np.float32).reshape(1, 1, 3)
-        v.active.fill_(True)  # the single drone never leaves the env
-        v.step(torch.as_tensor(a).to(v.device))
+        io, v = self._io, self._vec
+        io.h_in["actions"][0, 0] = np.asarray(action, np.float32).reshape(3)
+        io.h_in["active"][0, 0] = True  # the single drone never leaves the env
+        io.send()
+        v.step(v.actions_in)
         self.step_count += 1
-        obs = _host(v.obs[0, 0]).copy()
-        rew = float(_host(v.reward[0])[0])
-        fl = int(_host(v.info_flags[0])[0])
-        dist = float(_host(v.dist_goal[0])[0])
+        h = io.fetch()
+        obs = h["obs"][0, 0].copy()
+        rew = float(h["reward"][0, 0])
+        fl = int(h["info_flags"][0, 0])
+        dist = float(h["dist_goal"][0, 0])
         reached = bool(fl & nat.AGENT_REACHED)
         collision = bool(fl & nat.AGENT_COLLISION)
         terminated = bool(reached or collision)

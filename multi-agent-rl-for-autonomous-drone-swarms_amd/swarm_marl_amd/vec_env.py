@@ -47,7 +47,7 @@ class VecSwarm:
                  device: str | torch.device | None = None, with_infos: bool = False,
                  with_global_state: bool = False, physics: dict[str, Any] | None = None,
                  kernel_path: str = "auto", persistent: bool = True, waves_per_simd: int = 0,
-                 groups: int = 1):
+                 groups: int = 1, packed_io: bool = False):
         if isinstance(config, DroneEnvConfig):
             cfg, raw = config, {}
         else:
@@ -136,7 +136,23 @@ class VecSwarm:
         self.vel = torch.zeros((e, n, 3), dtype=f32, **kw)
         self.goal = torch.zeros((e, 3), dtype=f32, **kw)
         self.obstacles = torch.zeros((e, m, 3), dtype=f32, **kw)
-        self.active = torch.ones((e, n), dtype=torch.bool, **kw)
+        # packed_io (the dict-API envs): the per-step inputs (an actions buffer and the active
+        # mask) and all outputs are views of two flat device arenas, so that one step moves one
+        # H2D and one D2H copy (in_layout / out_layout: name -> (byte offset, shape, dtype))
+        self.packed_io = bool(packed_io)
+        self.in_arena = self.out_arena = None
+        self.in_layout, self.out_layout = {}, {}
+        if self.packed_io:
+            self.in_arena, views = self._arena(self.in_layout, [
+                ("actions", (e, n, 3), f32), ("active", (e, n), torch.bool),
+                ("action_mask", (e, n), torch.uint8)], self.device)
+            self.actions_in = views["actions"]
+            self.action_mask_in = views["action_mask"]
+            self.active = views["active"]
+            self.active.fill_(True)
+        else:
+            self.actions_in = self.action_mask_in = None
+            self.active = torch.ones((e, n), dtype=torch.bool, **kw)
         self.step_count = torch.zeros((e,), dtype=torch.int32, **kw)
         self.episode = torch.zeros((e,), dtype=torch.int32, **kw)  # read as uint32 by the kernel
         self.damping = torch.zeros((e, n), dtype=f32, **kw)
@@ -145,18 +161,46 @@ class VecSwarm:
         self.work = (torch.zeros((self.groups, nat.WORK_WORDS), dtype=torch.int32, **kw)
                      if self.persistent else None)
         # ---- outputs (persistent buffers)
-        self.obs = torch.zeros((e, n, d), dtype=f32, **kw)
-        self.reward = torch.zeros((e, n), dtype=f32, **kw)
-        self.terminated = torch.zeros((e, n), dtype=torch.bool, **kw)
-        self.truncated = torch.zeros((e, n), dtype=torch.bool, **kw)
-        self.env_done = torch.zeros((e,), dtype=torch.uint8, **kw)
-        self.dist_goal = torch.zeros((e, n), dtype=f32, **kw) if with_infos else None
-        self.info_flags = torch.zeros((e, n), dtype=torch.uint8, **kw) if with_infos else None
-        self.global_state = (torch.zeros((e, 6 * n + 3), dtype=f32, **kw)
-                             if with_global_state else None)
+        outs = [("obs", (e, n, d), f32), ("reward", (e, n), f32)]
+        if with_infos:
+            outs.append(("dist_goal", (e, n), f32))
+        if with_global_state:
+            outs.append(("global_state", (e, 6 * n + 3), f32))
+        outs += [("terminated", (e, n), torch.bool), ("truncated", (e, n), torch.bool),
+                 ("env_done", (e,), torch.uint8)]
+        if with_infos:
+            outs.append(("info_flags", (e, n), torch.uint8))
+        if self.packed_io:
+            self.out_arena, views = self._arena(self.out_layout, outs, self.device)
+        else:
+            views = {name: torch.zeros(shape, dtype=dt, **kw) for name, shape, dt in outs}
+        for name in ("obs", "reward", "terminated", "truncated", "env_done", "dist_goal",
+                     "info_flags", "global_state"):
+            setattr(self, name, views.get(name))
         self._bind()
 
     # ------------------------------------------------------------------ plumbing
+    @staticmethod
+    def _arena(layout: dict, fields, device):
+        """One zeroed uint8 buffer holding `fields` (name, shape, dtype) at 16-B aligned offsets;
+        returns (buffer, {name: typed view}) and fills `layout`."""
+        off = 0
+        for name, shape, dt in fields:
+            nbytes = torch.Size(shape).numel() * torch.empty((), dtype=dt).element_size()
+            layout[name] = (off, tuple(shape), dt)
+            off += (nbytes + 15) // 16 * 16
+        buf = torch.zeros((max(off, 16),), dtype=torch.uint8, device=device)
+        return buf, VecSwarm.arena_views(buf, layout)
+
+    @staticmethod
+    def arena_views(buf: torch.Tensor, layout: dict) -> dict:
+        """Typed views of an arena laid out by `layout` (device arena or a host mirror of it)."""
+        out = {}
+        for name, (off, shape, dt) in layout.items():
+            nbytes = torch.Size(shape).numel() * torch.empty((), dtype=dt).element_size()
+            out[name] = buf[off:off + nbytes].view(dt).view(shape)
+        return out
+
     def _bind(self) -> None:
         """ctypes state/out blocks per group: row `lo` of every [E, ...] tensor onwards."""
         def off(t, lo):

@@ -15,7 +15,7 @@ for c in ${CONFIGS:-headline n16 n256}; do
     d=gpurun_out/$R/pmc_$c/p$i
     mkdir -p $d
     echo "== $c pass $i: $set"
-    timeout -k 10 -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $d -o run -- python3 bench.py --config $c --steps 40 --warmup 5 --no-cpu-baseline > $d.log 2>&1
+    timeout -k 10 -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $d -o run -- python3 bench.py --config $c --groups 1 --steps 40 --warmup 5 --device-warmup-ms 0 --no-cpu-baseline > $d.log 2>&1
     rc=$?
     echo "rc=$rc"
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -n 5 $d.log; echo "STOP (rc=$rc)"; exit $rc; fi
