@@ -155,10 +155,13 @@ class PackedIO:
         return self.h_out
 
 
-def build_step_dicts(agent_ids, obs, rew, term, trunc, info_flags, dist, gs, env_done, env=None):
+def build_step_dicts(agent_ids, obs, rew, term, trunc, info_flags, dist, gs, env_done, env=None,
+                     gs_info=None):
     """Assemble the RLlib dicts from the kernel's dense outputs (drone_swarm_env.py:129-174).
 
-    Pure host logic on numpy arrays; `env.agents` is updated when an env is given.
+    Pure host logic on numpy arrays; `env.agents` is updated when an env is given.  Each info
+    gets its own copy of `gs` as "global_state" (like the reference), or the entries of
+    `gs_info` instead when given (e.g. a device-ring reference; {} for none).
     """
     rewards, terminated, truncated, infos, observations = {}, {}, {}, {}, {}
     nxt = []
@@ -173,8 +176,11 @@ def build_step_dicts(agent_ids, obs, rew, term, trunc, info_flags, dist, gs, env
             observations[a] = np.array(obs[i], dtype=np.float32)
             infos[a] = {"distance_to_goal": float(dist[i]),
                         "reached_goal": bool(fl & nat.AGENT_REACHED),
-                        "collision": bool(fl & nat.AGENT_COLLISION),
-                        "global_state": np.array(gs, dtype=np.float32)}
+                        "collision": bool(fl & nat.AGENT_COLLISION)}
+            if gs_info is None:
+                infos[a]["global_state"] = np.array(gs, dtype=np.float32)
+            else:
+                infos[a].update(gs_info)
             nxt.append(a)
     terminated["__all__"] = bool(env_done & nat.ENV_TERMINATED)
     truncated["__all__"] = bool(env_done & nat.ENV_TRUNCATED)
