@@ -240,6 +240,46 @@ int swarm_policy_forward(const swarm_policy_t* p, const float* obs, long long ro
 
 const char* swarm_policy_last_error(void);
 
+/*
+ * On-device evaluation metrics: the per-episode summary of
+ * scripts/evaluate_protocol.py:237-331 (`_run_single_episode_multi_agent`; formation error
+ * :103-116) accumulated on the device from a step's outputs (obs, reward, info_flags, env_done:
+ * the env must be stepped with infos).  swarm_eval_update after every swarm_step appends one
+ * record per finished episode; the host aggregates the records like `_aggregate` (:334-350).
+ * Replaces the host-side per-agent loop over the dict outputs of every evaluation step.
+ */
+#define SWARM_EVAL_LIVE 1u       /* status: an episode is being accumulated */
+#define SWARM_EVAL_COLLIDED 2u   /* status: an observed agent reported a collision */
+#define SWARM_EVAL_RECORD 8      /* doubles per record: global env index, success, collision_free, time_to_goal
+                                    (NaN if never all-reached), formation_error, path_efficiency,
+                                    episode_reward, steps */
+
+typedef struct swarm_eval {
+  double* ep_reward;      /* [E] sum over steps of the mean reward of the stepped agents */
+  int32_t* ep_steps;      /* [E] */
+  int32_t* reached_step;  /* [E] first step whose observed agents all reached (-1: none yet) */
+  uint8_t* status;        /* [E] SWARM_EVAL_* bits */
+  double* fe_sum;         /* [E] sum over steps of the formation error */
+  float* start;           /* [E,N,3] positions at the episode start */
+  float* goal;            /* [E,N,3] start + obs[6:9] (the reference's goal estimate) */
+  float* last;            /* [E,N,3] last observed positions */
+  double* traveled;       /* [E,N]   path length */
+  double* records;        /* [capacity, SWARM_EVAL_RECORD] finished episodes */
+  uint32_t* count;        /* [1] records appended (may exceed capacity: the rest are dropped) */
+  int32_t capacity;
+  int32_t reserved;
+} swarm_eval_t;
+
+/* Start an episode in the masked envs (all if NULL) from the current obs (after a reset). */
+int swarm_eval_begin(const swarm_params_t* p, const swarm_eval_t* ev, const swarm_out_t* out,
+                     const uint8_t* env_mask, void* hip_stream);
+
+/* Accumulate one step's outputs; close finished episodes (and open the next one of an env the
+ * step auto-reset).  Async on hip_stream, no allocation, no sync. */
+int swarm_eval_update(const swarm_params_t* p, const swarm_eval_t* ev, const swarm_out_t* out, void* hip_stream);
+
+const char* swarm_eval_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,12 +50,16 @@ POLICY_BF16 = 0
 POLICY_F32 = 1
 POLICY_ACT_MEAN = 0
 POLICY_ACT_SAMPLE = 1
+EVAL_LIVE = 1
+EVAL_COLLIDED = 2
+EVAL_RECORD = 8
 
 # every symbol include/swarm_mi355x.h declares
 EXPORTED_SYMBOLS = (
     "swarm_abi_version", "swarm_last_error", "swarm_params_default", "swarm_obs_dim",
     "swarm_query_launch", "swarm_step", "swarm_reset", "swarm_observe",
     "swarm_policy_packed_bytes", "swarm_policy_pack", "swarm_policy_forward", "swarm_policy_last_error",
+    "swarm_eval_begin", "swarm_eval_update", "swarm_eval_last_error",
 )
 
 
@@ -118,6 +122,12 @@ class SwarmPolicy(ctypes.Structure):
                 ("reserved", ctypes.c_int32), ("weights", ctypes.c_void_p)]
 
 
+class SwarmEval(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name in
+                ("ep_reward", "ep_steps", "reached_step", "status", "fe_sum", "start", "goal", "last",
+                 "traveled", "records", "count")] + [("capacity", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
 class SwarmLaunchInfo(ctypes.Structure):
     _fields_ = [(name, ctypes.c_int32) for name in
                 ("threads_per_block", "envs_per_block", "lanes_per_env", "blocks", "lds_bytes",
@@ -168,6 +178,13 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
                                          ctypes.c_ulonglong, ctypes.c_ulonglong, vp]
     lib.swarm_policy_last_error.restype = ctypes.c_char_p
     lib.swarm_policy_last_error.argtypes = []
+    ev = ctypes.POINTER(SwarmEval)
+    lib.swarm_eval_begin.restype = ctypes.c_int
+    lib.swarm_eval_begin.argtypes = [P, ev, O, vp, vp]
+    lib.swarm_eval_update.restype = ctypes.c_int
+    lib.swarm_eval_update.argtypes = [P, ev, O, vp]
+    lib.swarm_eval_last_error.restype = ctypes.c_char_p
+    lib.swarm_eval_last_error.argtypes = []
     got = lib.swarm_abi_version()
     if got != ABI_VERSION:
         raise NativeLibraryError(f"{p}: ABI version {got}, expected {ABI_VERSION}")
@@ -176,12 +193,14 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     return lib
 
 
-def check(rc: int, lib: ctypes.CDLL | None = None, policy: bool = False) -> None:
-    """Raise on a negative return code (bad arguments -> ValueError, HIP errors -> RuntimeError)."""
+def check(rc: int, lib: ctypes.CDLL | None = None, policy: bool = False, which: str | None = None) -> None:
+    """Raise on a negative return code (bad arguments -> ValueError, HIP errors -> RuntimeError).
+    `which` names the component whose last-error string explains it ("policy", "eval")."""
     if rc == SWARM_OK:
         return
     lib = lib or load_library()
-    err = lib.swarm_policy_last_error if policy else lib.swarm_last_error
+    which = "policy" if policy else which
+    err = {"policy": lib.swarm_policy_last_error, "eval": lib.swarm_eval_last_error}.get(which, lib.swarm_last_error)
     msg = (err() or b"").decode(errors="replace")
     if rc in (SWARM_EINVAL, SWARM_ENULL, SWARM_ELIMIT):
         raise ValueError(f"swarm_mi355x error {rc}: {msg}")

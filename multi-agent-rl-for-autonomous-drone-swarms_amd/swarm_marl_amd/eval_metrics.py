@@ -1,0 +1,127 @@
+"""On-device evaluation metrics for a VecSwarm.
+
+The reference evaluates one episode at a time on the host: scripts/evaluate_protocol.py:237-331
+walks the dict outputs of every step (path length, formation error, collision / all-reached
+votes, reward) and :334-350 aggregates the episode summaries into success rate (SR),
+collision-free rate (CFR), mean time to goal (TTG), formation error (FE), path efficiency (PE)
+and the reward mean / std.  `EvalTracker` accumulates the same per-episode quantities on the
+device for all E envs at once (swarm_eval_update, one launch after each step, no host sync) and
+aggregates the finished-episode records on the host exactly like `_aggregate`:
+
+    vec = VecSwarm(E, cfg, with_infos=True, auto_reset=True); vec.reset()
+    ev = EvalTracker(vec); ev.begin()
+    for t in range(T):
+        vec.step(policy(vec.obs)); ev.update()
+    ev.aggregate()   # {"success_rate": ..., "collision_free_rate": ..., ...}
+
+Semantics kept from the reference, including that the terminal step (no observations,
+drone_swarm_env.py:154) counts as "all reached" and carries no collision vote.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from statistics import mean, pstdev
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .vec_env import VecSwarm
+
+FIELDS = ("env", "success", "collision_free", "time_to_goal", "formation_error", "path_efficiency",
+          "episode_reward", "steps")
+
+
+def aggregate_records(rec: np.ndarray) -> dict:
+    """evaluate_protocol.py:334-350 `_aggregate` over records [n, 8] (FIELDS order)."""
+    if len(rec) == 0:
+        return {"episodes": 0, "success_rate": 0.0, "collision_free_rate": 0.0, "mean_time_to_goal": math.nan,
+                "formation_error": 0.0, "path_efficiency": 0.0, "episode_reward_mean": 0.0,
+                "episode_reward_std": 0.0}
+    ttg = [float(x) for x in rec[:, 3] if not math.isnan(x)]
+    rw = [float(x) for x in rec[:, 6]]
+    return {"episodes": int(len(rec)),
+            "success_rate": float(mean(int(x) for x in rec[:, 1])),
+            "collision_free_rate": float(mean(int(x) for x in rec[:, 2])),
+            "mean_time_to_goal": float(mean(ttg)) if ttg else math.nan,
+            "formation_error": float(mean(float(x) for x in rec[:, 4])),
+            "path_efficiency": float(mean(float(x) for x in rec[:, 5])),
+            "episode_reward_mean": float(mean(rw)),
+            "episode_reward_std": float(pstdev(rw)) if len(rw) > 1 else 0.0}
+
+
+class EvalTracker:
+    def __init__(self, vec: VecSwarm, capacity: int = 65536):
+        if vec.info_flags is None:
+            raise ValueError("EvalTracker needs a VecSwarm built with with_infos=True")
+        if vec.dynamics != "kinematic":
+            raise ValueError("EvalTracker follows the kinematic swarm protocol (evaluate_protocol.py)")
+        self.vec = vec
+        self.lib = vec.lib
+        e, n, dev = vec.num_envs, vec.num_drones, vec.device
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.ep_reward = torch.zeros(e, **f64)
+        self.ep_steps = torch.zeros(e, dtype=torch.int32, device=dev)
+        self.reached_step = torch.full((e,), -1, dtype=torch.int32, device=dev)
+        self.status = torch.zeros(e, dtype=torch.uint8, device=dev)
+        self.fe_sum = torch.zeros(e, **f64)
+        self.start = torch.zeros((e, n, 3), dtype=torch.float32, device=dev)
+        self.goal = torch.zeros_like(self.start)
+        self.last = torch.zeros_like(self.start)
+        self.traveled = torch.zeros((e, n), **f64)
+        self.capacity = int(capacity)
+        self.records_buf = torch.zeros((max(self.capacity, 1), nat.EVAL_RECORD), **f64)
+        self.count = torch.zeros(1, dtype=torch.int32, device=dev)
+        c = nat.SwarmEval()
+        for name in ("ep_reward", "ep_steps", "reached_step", "status", "fe_sum", "start", "goal", "last",
+                     "traveled", "count"):
+            setattr(c, name, getattr(self, name).data_ptr())
+        c.records = self.records_buf.data_ptr()
+        c.capacity = self.capacity
+        self._c = c
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.vec.device).cuda_stream
+
+    def begin(self, env_mask: torch.Tensor | None = None) -> None:
+        """Open an episode in the masked envs (all if None) from the current observations."""
+        self.vec.join()
+        mp = self.vec._mask_ptr(env_mask)
+        for g, (lo, _) in enumerate(self.vec.group_slices):
+            nat.check(self.lib.swarm_eval_begin(ctypes.byref(self.vec._gparams[g]), ctypes.byref(self._group_c(g)),
+                                                ctypes.byref(self.vec._gout[g]), None if mp is None else mp + lo,
+                                                self._stream()), self.lib, which="eval")
+
+    def update(self) -> None:
+        """Accumulate the last step (call after every VecSwarm.step)."""
+        self.vec.join()
+        for g in range(self.vec.groups):
+            nat.check(self.lib.swarm_eval_update(ctypes.byref(self.vec._gparams[g]), ctypes.byref(self._group_c(g)),
+                                                 ctypes.byref(self.vec._gout[g]), self._stream()), self.lib,
+                      which="eval")
+
+    def _group_c(self, g: int) -> nat.SwarmEval:
+        if self.vec.groups == 1:
+            return self._c
+        lo = self.vec.group_slices[g][0]
+        c = nat.SwarmEval()
+        for name in ("ep_reward", "ep_steps", "reached_step", "status", "fe_sum", "start", "goal", "last",
+                     "traveled"):
+            t = getattr(self, name)
+            setattr(c, name, t.data_ptr() + lo * t.stride(0) * t.element_size())
+        c.records, c.count, c.capacity = self.records_buf.data_ptr(), self.count.data_ptr(), self.capacity
+        return c
+
+    def records(self) -> np.ndarray:
+        """Finished-episode records [n, 8] (FIELDS), in completion order."""
+        n = int(self.count.item())
+        if n > self.capacity:
+            raise RuntimeError(f"{n} episodes finished but the record buffer holds {self.capacity}")
+        return self.records_buf[:n].cpu().numpy()
+
+    def aggregate(self) -> dict:
+        return aggregate_records(self.records())
+
+    def clear(self) -> None:
+        self.count.zero_()

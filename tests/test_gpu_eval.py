@@ -1,0 +1,136 @@
+"""GPU: on-device eval metrics (swarm_eval_update / EvalTracker) against the reference's metric
+code and its restatement.
+
+* Every episode of tests/golden/eval_*.npz (the reference's evaluate_protocol.py metric functions
+  on the reference DroneSwarmEnv, make_eval_golden.py) is replayed as one env of a VecSwarm from
+  its recorded reset state and actions: success, collision-free and time-to-goal exact,
+  formation error and path efficiency to 1e-9 relative, episode reward within the per-step
+  reward contract (1e-5 x steps), and the `_aggregate` dict.
+* With in-kernel auto-reset (episodes rolling over inside the launch), every record equals the
+  oracle's (oracle/eval_oracle.py) summary of the same env's episode, fed the dict outputs.
+"""
+from __future__ import annotations
+
+import json
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+EVAL_FIXTURES = sorted(p.name for p in GOLDEN.glob("eval_*.npz"))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+def _cmp_summary(got, exp, steps, tag):
+    assert got[1] == exp[0] and got[2] == exp[1], tag
+    assert (math.isnan(got[3]) and math.isnan(exp[2])) or got[3] == exp[2], tag
+    assert got[4] == pytest.approx(exp[3], rel=1e-9, abs=1e-12), tag
+    assert got[5] == pytest.approx(exp[4], rel=1e-9, abs=1e-12), tag
+    assert abs(got[6] - exp[5]) <= 1e-5 * steps + 1e-9, tag
+
+
+@pytest.mark.parametrize("name", EVAL_FIXTURES)
+def test_eval_replays_reference_episodes(dev, name):
+    from swarm_marl_amd import VecSwarm
+    from swarm_marl_amd.eval_metrics import EvalTracker
+    d = np.load(GOLDEN / name)
+    cfg = json.loads(str(d["config"]))
+    n = int(cfg["num_drones"])
+    lens = d["lengths"]
+    e = len(lens)
+    vec = VecSwarm(e, cfg, device=dev, auto_reset=False, with_infos=True)
+    vec.set_state(pos=d["reset_pos"], vel=np.zeros((e, n, 3), np.float32), goal=d["reset_goal"],
+                  obstacles=d["reset_obst"], active=np.ones((e, n), bool), step_count=np.zeros(e, np.int32))
+    vec.observe()
+    ev = EvalTracker(vec, capacity=64)
+    ev.begin()
+    acts = torch.as_tensor(d["actions"], device=dev)
+    for t in range(int(lens.max()) + 2):  # two steps past the last end: finished envs stay closed
+        vec.step(acts[:, t].contiguous() if t < acts.shape[1] else torch.zeros((e, n, 3), device=dev))
+        ev.update()
+    rec = ev.records()
+    assert len(rec) == e
+    rec = rec[np.argsort(rec[:, 0], kind="stable")]
+    for k in range(e):
+        assert int(rec[k, 7]) == int(lens[k])
+        _cmp_summary(rec[k], d["summaries"][k], int(lens[k]), (name, k))
+    agg, ref = ev.aggregate(), json.loads(str(d["aggregate"]))
+    for key in ("success_rate", "collision_free_rate", "mean_time_to_goal"):
+        assert agg[key] == ref[key], key
+    for key in ("formation_error", "path_efficiency"):
+        assert agg[key] == pytest.approx(ref[key], rel=1e-9), key
+    assert agg["episode_reward_mean"] == pytest.approx(ref["episode_reward_mean"], abs=1e-3)
+
+
+def test_eval_auto_reset_matches_oracle(dev):
+    from oracle import eval_oracle as ev_o
+    from swarm_marl_amd import VecSwarm
+    from swarm_marl_amd import _native as nat
+    from swarm_marl_amd.envs.drone_swarm_env import build_step_dicts
+    from swarm_marl_amd.eval_metrics import EvalTracker
+    e, n, steps = 96, 8, 60
+    vec = VecSwarm(e, {"num_drones": n, "max_steps": 25}, device=dev, auto_reset=True, seed=5, with_infos=True,
+                   with_global_state=True, groups=2)
+    vec.reset()
+    ev = EvalTracker(vec, capacity=4096)
+    ev.begin()
+    ids = [f"drone_{i}" for i in range(n)]
+
+    def reset_obs(o, i):
+        return {a: o[i, k].copy() for k, a in enumerate(ids)}
+
+    obs0 = vec.obs.cpu().numpy()
+    trackers = [ev_o.EpisodeMetrics(reset_obs(obs0, i), 2.5) for i in range(e)]
+    expected = []
+    g = torch.Generator(device=dev).manual_seed(9)
+    for t in range(steps):
+        vec.step(torch.rand((e, n, 3), device=dev, generator=g) * 2 - 1)
+        ev.update()
+        o, r = vec.obs.cpu().numpy(), vec.reward.cpu().numpy()
+        te, tr = vec.terminated.cpu().numpy(), vec.truncated.cpu().numpy()
+        fl, dg = vec.info_flags.cpu().numpy(), vec.dist_goal.cpu().numpy()
+        gs, done = vec.global_state.cpu().numpy(), vec.env_done.cpu().numpy()
+        for i in range(e):
+            outs = build_step_dicts(ids, o[i], r[i], te[i], tr[i], fl[i], dg[i], gs[i], int(done[i]))
+            if trackers[i].update(*outs):
+                expected.append((i, trackers[i].summary(), trackers[i].steps))
+                assert done[i] & nat.ENV_RESET
+                trackers[i] = ev_o.EpisodeMetrics(reset_obs(o, i), 2.5)
+    rec = ev.records()
+    assert len(rec) == len(expected) > 0
+    got = {}
+    for row in rec:
+        got.setdefault(int(row[0]), []).append(row)
+    for i, s, st in expected:
+        row = got[i].pop(0)
+        assert int(row[7]) == st
+        _cmp_summary(row, s, st, i)
+
+
+def test_curriculum_runner_stages(dev):
+    from swarm_marl_amd.curriculum import CurriculumRunner
+    from tests.test_eval_cpu import STAGES
+    run = CurriculumRunner(STAGES, 32, base_seed=3, device=dev)
+    seen = []
+    while not run.done:
+        v = run.vec
+        seen.append((v.num_drones, int(v.cfg.num_obstacles)))
+        g = torch.Generator(device=dev).manual_seed(run.index)
+        while not run.ready():
+            for _ in range(40):
+                run.step(torch.rand((32, v.num_drones, 3), device=dev, generator=g) * 2 - 1)
+            run.end_iteration()
+        m = run.window_metrics()
+        assert m["episodes"] > 0 and 0.0 <= m["success_rate"] <= 1.0
+        run.advance()
+    assert seen == [(3, 0), (5, 4)]
