@@ -101,6 +101,7 @@ struct KParams {
   int E, N, M, K, Ms, D, max_steps, auto_reset, substeps, damping_law;
   int log2_lanes, envs_per_block, chunk_rows, obs_vec4, pack_bytes;
   int off_obst, off_stage, obst_stride, ring;   // ring: pos4 slots per team (2L wave, L block)
+  int off_pair;   // block teams with N a power of two: pair-entry ring (BLK_PAIR_STRIDE floats x 2N)
   uint32_t nb_keep, ob_keep;        // key masks: high bits kept from the distance, low bits = index
   long long env_offset;
   unsigned seed_lo, seed_hi;
@@ -400,6 +401,72 @@ __device__ __forceinline__ void pair_pass_block(const float4* __restrict__ pos4,
   }
 }
 
+// Block teams (one env per workgroup, N a power of two > 64), every drone eligible: rotation pass
+// j = t + r (r = 1 .. N-1) over a ring of pair entries — entry j holds drones j and j+1 (mod N)
+// as (x_j, x_j+1, y_j, y_j+1, z_j, z_j+1, pad): one ds_read2_b32 per coordinate feeds the
+// packed-f32 distances of rotations r and r+1 (7-float stride: conflict-free lanes).  Keys carry
+// the rotation offset (decoded as (t + r) & (N-1), like the wave teams), so no self-pair select;
+// formation terms are summed in f32 per 8 pairs then in f64.  Same values as pair_pass_block.
+constexpr int BLK_PAIR_STRIDE = 7;
+typedef float blk_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void blk_put_pair(float* __restrict__ pr, int N, int t, float px, float py, float pz) {
+  // drone t is the first half of entries t, t+N and the second half of entries t-1, t-1+N
+  const int a = t, b = (t + N - 1) & (N - 1);
+  float* e0 = pr + a * BLK_PAIR_STRIDE;
+  float* e1 = pr + (a + N) * BLK_PAIR_STRIDE;
+  float* e2 = pr + b * BLK_PAIR_STRIDE + 1;
+  float* e3 = pr + (b + N) * BLK_PAIR_STRIDE + 1;
+  e0[0] = px; e0[2] = py; e0[4] = pz;
+  e1[0] = px; e1[2] = py; e1[4] = pz;
+  e2[0] = px; e2[2] = py; e2[4] = pz;
+  e3[0] = px; e3[2] = py; e3[4] = pz;
+}
+// KEYS = false (the step's first pass of a block team): formation terms and the running minimum
+// of d~ only — the keys follow in a PASS 0 pass once the env is known not to reset (at N >= 128
+// almost every env resets every step, and a reset env's keys come from its new positions).
+template <int KS, int PASS, bool KEYS = true>
+__device__ __forceinline__ void pair_pass_block_fast(const float* __restrict__ pr, int N, int t, float px, float py,
+                                                     float pz, uint32_t keep, float ds,
+                                                     uint32_t (&nk)[KS > 0 ? KS : 1], double& fsum,
+                                                     float& vmin) {
+  const float* q = pr + t * BLK_PAIR_STRIDE;
+  float esum = 0.f;
+  int r = 1;
+#pragma unroll 4
+  for (; r + 1 < N; r += 2) {
+    const float* e = q + r * BLK_PAIR_STRIDE;
+    const blk_f2 X = {e[0], e[1]}, Y = {e[2], e[3]}, Z = {e[4], e[5]};
+    const blk_f2 dx = X - px, dy = Y - py, dz = Z - pz;
+    blk_f2 sq = dx * dx;
+    sq = __builtin_elementwise_fma(dy, dy, sq);
+    sq = __builtin_elementwise_fma(dz, dz, sq);
+    const float va = pair_value<PASS>(sq.x), vb = pair_value<PASS>(sq.y);
+    if constexpr (KS > 0 && KEYS) {
+      kins<KS>(nk, (__float_as_uint(va) & keep) | (uint32_t)r);
+      kins<KS>(nk, (__float_as_uint(vb) & keep) | (uint32_t)(r + 1));
+    }
+    if constexpr (!KEYS) vmin = fminf(vmin, fminf(va, vb));
+    if constexpr (PASS == 1) {
+      const blk_f2 V = {va, vb};
+      const blk_f2 Ed = V - ds;
+      esum += fabsf(Ed.x);
+      esum += fabsf(Ed.y);
+      if ((r & 7) == 7) {
+        fsum += (double)esum;
+        esum = 0.f;
+      }
+    }
+  }
+  if (r < N) {  // N - 1 is odd: the last rotation alone
+    const float* e = q + r * BLK_PAIR_STRIDE;
+    const float v = pair_value<PASS>(sqsum_rank(e[0] - px, e[2] - py, e[4] - pz));
+    if constexpr (KS > 0 && KEYS) kins<KS>(nk, (__float_as_uint(v) & keep) | (uint32_t)r);
+    if constexpr (!KEYS) vmin = fminf(vmin, v);
+    if constexpr (PASS == 1) esum += fabsf(v - ds);
+  }
+  if constexpr (PASS == 1) fsum += (double)esum;
+}
+
 template <int MSL, bool COLL>
 __device__ __forceinline__ void obstacle_pass(const float4* __restrict__ obst4, int M, float px, float py, float pz,
                                               bool chk, float s_thr, uint32_t keep,
@@ -575,6 +642,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   float4* ring = reinterpret_cast<float4*>(smem) + team * P.ring;
   float4* obst4 = reinterpret_cast<float4*>(smem + P.off_obst) + team * P.obst_stride;
   float* stage = reinterpret_cast<float*>(smem + P.off_stage);
+  float* pair_ring = reinterpret_cast<float*>(smem + P.off_pair);  // block teams, P.off_pair > 0
   uint64_t team_bits = 0;
   // one env of exactly 64 agents per wave: the per-agent byte outputs (terminated, truncated,
   // active) leave as three 64-B dword stores built from wave ballots instead of 3 x 64 byte stores
@@ -719,6 +787,9 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   auto put_ring = [&](float w) {
     ring[t] = make_float4(px, py, pz, w);
     if constexpr (WAVE) ring[t + L] = make_float4(px, py, pz, w);
+    if constexpr (!WAVE) {
+      if (P.off_pair > 0 && t < N) blk_put_pair(pair_ring, N, t, px, py, pz);
+    }
   };
 
   if (mode == MODE_RESET && sel) {  // explicit device reset: draw before the observation pass
@@ -749,6 +820,9 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   // all-eligible fast path: wave-uniform, needs the nearest neighbour (KS > 0) and no padding
   bool fast = false;
   if constexpr (WAVE) fast = (KS > 0) && (N == L) && __all(elig);
+  // block teams: the rotation pass over the pair-entry ring (N a power of two, kinematic)
+  if constexpr (!WAVE && KS > 0 && DYN == DYN_KIN) fast = P.off_pair > 0 && __syncthreads_and(!is_agent || elig) != 0;
+  const bool blk_rot = !WAVE && P.off_pair > 0;  // aux / reset passes of block teams rotate too
   if (pass_env && !(SWARM_ABLATE & ABL_PAIR)) {
     if (mode == MODE_STEP) {
       constexpr int PASS = (DYN == DYN_KIN) ? 1 : 2;
@@ -763,7 +837,12 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
             pair_pass_wave<KS, PASS, false>(ring, L, t, tid, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
         }
       } else {
-        pair_pass_block<KS, PASS>(ring, N, t, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
+        if constexpr (DYN == DYN_KIN) {
+          if (fast) pair_pass_block_fast<KS, PASS, false>(pair_ring, N, t, px, py, pz, P.nb_keep, P.ds_f, nk, fsum, smin);
+          else pair_pass_block<KS, PASS>(ring, N, t, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
+        } else {
+          pair_pass_block<KS, PASS>(ring, N, t, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
+        }
       }
       if constexpr (SWARM_ABLATE & ABL_OBST) {}
       else if constexpr (DYN == DYN_KIN) obstacle_pass<MSL, true>(obst4, M, px, py, pz, act, P.s_obst, P.ob_keep, ok, ocoll);
@@ -773,7 +852,8 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         if constexpr (W64 && !(SWARM_ABLATE & ABL_W64)) pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
         else pair_pass_wave<KS, 0, true>(ring, L, t, tid, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
       } else {
-        pair_pass_block<KS, 0>(ring, N, t, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
+        if (blk_rot) pair_pass_block_fast<KS, 0>(pair_ring, N, t, px, py, pz, P.nb_keep, 0.f, nk, fsum, smin);
+        else pair_pass_block<KS, 0>(ring, N, t, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
       }
       obstacle_pass<MSL, false>(obst4, M, px, py, pz, false, 0.f, P.ob_keep, ok, ocoll);
     }
@@ -787,13 +867,15 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   for (int s = 0; s < NW; ++s) { wd[s] = 0.f; wj[s] = 0x7fffffff; }
 #pragma unroll
   for (int s = 0; s < OW; ++s) { od[s] = 0.f; oj[s] = 0x7fffffff; }
-  const int imod = WAVE ? (L - 1) : 0x7fffffff;
-  const int Kq = (fast && K < 1) ? 1 : K;  // the fast collision test needs the nearest
+  // neighbour keys carry the rotation offset (wave teams, block rotation passes: `rot`) or the
+  // drone index (block pair_pass_block)
+  const int Kq = K;
   const int Mse = Ms < M ? Ms : M;
-  auto select_topk = [&](bool run, bool dkey) {
+  auto select_topk = [&](bool run, bool dkey, bool rot) {
     bool slow_nb = false, slow_ob = false;
     if (run && !(SWARM_ABLATE & ABL_FINISH)) {
-      if constexpr (KS > 0) slow_nb = !finish_keys<KS, false, true>(nk, ring, N, WAVE ? t : 0, imod, Kq, P.nb_keep, dkey, px, py, pz, wd, wj);
+      const int imod = rot ? (L - 1) : 0x7fffffff;
+      if constexpr (KS > 0) slow_nb = !finish_keys<KS, false, true>(nk, ring, N, rot ? t : 0, imod, Kq, P.nb_keep, dkey, px, py, pz, wd, wj);
       if constexpr (MSL > 0) slow_ob = !finish_keys<MSL, true, false>(ok, obst4, M, 0, 0x7fffffff, Mse, P.ob_keep, false, px, py, pz, od, oj);
     }
     if constexpr (KS > 0) {
@@ -803,8 +885,10 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       if (slow_ob) exact_select<OW, true>(obst4, M, -1, Mse, max_first(od, Mse), px, py, pz, od, oj);
     }
   };
-  // the step's kinematic pass ranks by d~, every other pass by s'
-  select_topk(is_agent && pass_env, KIND == KIND_STEP && DYN == DYN_KIN);
+  // the step's kinematic pass ranks by d~, every other pass by s'.  A step runs the finish only
+  // for the observation it emits (after the reset decision: a resetting env finishes once, for
+  // its new episode); reset / observe run it now.
+  if (mode != MODE_STEP) select_topk(is_agent && pass_env, false, WAVE || blk_rot);
   STAMP(4);
 
   // ---- rewards / terminations (step)
@@ -819,8 +903,13 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       const float s_exact_thr = (DYN == DYN_KIN) ? P.s_pair : P.s_phys_pair;
       const float d_thr = (DYN == DYN_KIN) ? P.thr_pair : P.thr_ppair;
       bool pcoll;
-      if (fast) {
-        pcoll = wd[0] <= d_thr;
+      if (fast && WAVE) {
+        // the nearest key bounds the exact nearest distance (d~ keys: kinematic; s' keys:
+        // physics): [key & keep, key | ~keep] x [FAST_LO, FAST_HI]; exact scan inside the band
+        const float thr = (DYN == DYN_KIN) ? d_thr : s_exact_thr;
+        pcoll = __uint_as_float(nk[0] | ~P.nb_keep) * FAST_HI <= thr;
+        if (!pcoll && __uint_as_float(nk[0] & P.nb_keep) * FAST_LO <= thr)
+          pcoll = exact_pair_collision(ring, N, t, px, py, pz, s_exact_thr);
       } else {
         // smin holds d~ (kinematic) or s' (physics): certain below the band, exact inside it
         const float band_thr = (DYN == DYN_KIN) ? d_thr : s_exact_thr;
@@ -898,6 +987,16 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       cont = true;
     }
     do_reset = P.auto_reset && env_ok && (term_all || trunc_all) && !(SWARM_ABLATE & ABL_RESET);
+    bool dkey_step = DYN == DYN_KIN;
+    if constexpr (!WAVE && DYN == DYN_KIN) {
+      if (fast && !do_reset) {  // block uniform: the keys of the emitted observation
+        float s3 = 0.f;
+        double f3 = 0.0;
+        pair_pass_block_fast<KS, 0>(pair_ring, N, t, px, py, pz, P.nb_keep, 0.f, nk, f3, s3);
+        dkey_step = false;  // PASS 0 keys rank by s'
+      }
+    }
+    select_topk(is_agent && !do_reset, dkey_step, WAVE || fast);
 
     // per-agent step outputs (the episode that just ended, for reset envs)
     if (is_agent) {
@@ -938,10 +1037,14 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         if constexpr (WAVE) {
           if constexpr (W64 && !(SWARM_ABLATE & ABL_W64)) pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
           else pair_pass_wave<KS, 0, true>(ring, L, t, tid, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
-        } else pair_pass_block<KS, 0>(ring, N, t, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
+        } else if (blk_rot) {
+          pair_pass_block_fast<KS, 0>(pair_ring, N, t, px, py, pz, P.nb_keep, 0.f, nk, f2, s2);
+        } else {
+          pair_pass_block<KS, 0>(ring, N, t, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
+        }
         obstacle_pass<MSL, false>(obst4, M, px, py, pz, false, 0.f, P.ob_keep, ok, c2);
       }
-      select_topk(do_reset && is_agent, false);
+      select_topk(do_reset && is_agent, false, WAVE || blk_rot);
     }
   } else if (sel && is_agent) {
     dist_out = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
@@ -2038,6 +2141,11 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   k.off_obst = G * k.ring * 16;
   const long long obst_bytes = (long long)G * k.obst_stride * 16;
   k.off_stage = (int)(k.off_obst + obst_bytes);
+  k.off_pair = 0;
+  if (!wave && lanes == k.N) {  // block team, N a power of two: the rotation passes' pair ring
+    k.off_pair = k.off_stage;
+    k.off_stage = (int)(k.off_pair + 2LL * k.N * BLK_PAIR_STRIDE * 4);
+  }
   const int rows = G * k.N;
   const long long row_bytes = 4LL * k.D;
   int rounds = (int)((rows * row_bytes + STAGE_BUDGET - 1) / STAGE_BUDGET);

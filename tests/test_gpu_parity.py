@@ -202,3 +202,30 @@ def test_tie_heavy_lattice(dev, n, k, ms, m):
         torch.cuda.synchronize()
         st, out = so.step(cfg, st, a, None, auto_reset=False, seed=2, exact_formation=True)
         _compare_step(vec, out, st, f"lattice N={n} K={k} Ms={ms} M={m} t={t}")
+
+
+@pytest.mark.parametrize("n,e,radii", [(128, 6, 0.0), (256, 3, 0.0), (256, 4, 0.5), (512, 2, 0.0), (128, 5, 0.5)])
+def test_block_rotation_passes_vs_oracle(dev, n, e, radii):
+    """Block teams with N a power of two run the rotation passes over the pair-entry ring: the
+    step's formation/minimum pass, then (envs that do not reset) a keys pass, or the reset's
+    keys pass.  radii 0 (no collisions, no goals: no resets until max_steps) exercises the
+    continuing path; default radii the reset path."""
+    from oracle import swarm_oracle as so
+    raw = dict(num_drones=n, max_steps=6, collision_radius=radii, goal_radius=radii,
+               obstacle_radius=radii if radii else 0.0)
+    cfg = oracle_cfg(raw)
+    vec = _vec(dev, raw, e, auto_reset=True, seed=17, env_offset=3)
+    vec.reset()
+    torch.cuda.synchronize()
+    st = vec_state_numpy(vec)
+    rng = np.random.default_rng(n + e)
+    resets = 0
+    for t in range(8):
+        a = rng.uniform(-1.2, 1.2, (e, n, 3)).astype(np.float32)
+        vec.step(torch.as_tensor(a).to(dev))
+        torch.cuda.synchronize()
+        st, out = so.step(cfg, st, a, None, auto_reset=True, seed=17, env_offset=3, exact_formation=(n * e <= 20000))
+        _compare_step(vec, out, st, f"N={n} E={e} radii={radii} t={t}")
+        resets += int((vec.env_done.cpu().numpy() & 4).astype(bool).sum())
+    if radii == 0.0:
+        assert resets == e  # only the max_steps truncation at t = 5

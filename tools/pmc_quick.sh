@@ -12,7 +12,7 @@ for set in \
   d=gpurun_out/$T/pmc_$C/p$i
   mkdir -p $d
   echo "== $C pass $i"
-  timeout -k 10 -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $d -o run -- python3 bench.py --config $C --steps 40 --warmup 5 --no-cpu-baseline > $d.log 2>&1
+  timeout -k 10 -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $d -o run -- python3 bench.py --config $C --groups 1 --device-warmup-ms 0 --steps 40 --warmup 5 --no-cpu-baseline > $d.log 2>&1
   rc=$?
   echo "rc=$rc"
   if [ $rc -ne 0 ]; then tail -n 5 $d.log; echo "STOP (rc=$rc)"; exit $rc; fi
