@@ -42,7 +42,10 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "agent-steps/sec at N=64 × E=8192 envs, 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-VALU_PEAK_LANE_OPS = 78.6e12  # f32 VALU lane-ops/s (157.3 TFLOP/s counting FMA as 2); SURVEY §8d
+# VALU issue peak in instruction-lanes/s: one wave64 VALU instruction per 4 cycles per SIMD
+# (16 lanes/clk) x 1024 SIMDs x 2.4 GHz.  The 157.3 TFLOP/s f32 spec counts a packed FMA as 4
+# FLOPs per lane (MI355X_MICROARCH.md: 64 FLOP/clk/SIMD); SQ_INSTS_VALU x 64 counts instruction-lanes.
+VALU_PEAK_LANE_OPS = 39.3e12
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA peaks, MI355X_MICROARCH.md
 
 # BASELINE.json configs, per GPU: [2] is the headline (the metric's config), [1] and [4] have
@@ -490,7 +493,8 @@ def main(argv=None):
             roof["valu"] = {"achieved_lane_ops_per_s": lane_ops / (kern_max * 1e-3),
                             "peak": VALU_PEAK_LANE_OPS,
                             "frac": lane_ops / (kern_max * 1e-3) / VALU_PEAK_LANE_OPS,
-                            "source": "SQ_INSTS_VALU x 64 lanes from profiles/pmc_traffic.json"}
+                            "source": "SQ_INSTS_VALU x 64 lanes from profiles/pmc_traffic.json; peak = "
+                                      "16 lanes/clk/SIMD x 1024 SIMDs x 2.4 GHz"}
         metric = METRIC if pol is None else \
             "rollout agent-steps/sec (on-device policy + env step) at N=64 x E=8192 per MI355X"
         rec = {
