@@ -68,6 +68,8 @@ def parse(argv=None):
     ap.add_argument("--config", choices=sorted(PRESETS), default="headline")
     ap.add_argument("--drones", type=int, default=None)
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU")
+    ap.add_argument("--dynamics", choices=("kinematic", "physics"), default="kinematic",
+                    help="physics = the point-mass restatement of DronePhysicsEnv (parity unpinned)")
     ap.add_argument("--no-term", action="store_true",
                     help="no-termination variant (collision/goal radii 0)")
     ap.add_argument("--ring", type=int, default=8, help="distinct pre-generated action tensors")
@@ -168,7 +170,7 @@ def _cpu_cores() -> tuple[int, str]:
     return aff, f"{aff} threads = every core of the affinity set"
 
 
-def cpu_baseline_port(n: int, e: int, seconds: float, raw: dict) -> dict:
+def cpu_baseline_port(n: int, e: int, seconds: float, raw: dict, physics: bool = False) -> dict:
     """C port of the reference step (oracle/swarm_oracle.c, OpenMP) on the benched workload:
     same N and E, auto-reset on, persistent buffers, a bounded number of steps."""
     from oracle import c_oracle as co
@@ -176,7 +178,7 @@ def cpu_baseline_port(n: int, e: int, seconds: float, raw: dict) -> dict:
 
     cores, why = _cpu_cores()
     cfg = so.make_cfg(**raw)
-    run = co.Runner(cfg, e, seed=0, nthreads=cores)
+    run = co.Runner(cfg, e, seed=0, nthreads=cores, physics=physics)
     rng = np.random.default_rng(1000)
     ring = [rng.uniform(-1, 1, (e, n, 3)).astype(np.float32) for _ in range(4)]
     run.step(ring[0])  # warm
@@ -188,9 +190,11 @@ def cpu_baseline_port(n: int, e: int, seconds: float, raw: dict) -> dict:
         if el >= seconds:
             break
     return {"value": e * n * steps / el, "unit": "agent-steps/s", "cores": cores, "kind": "port",
-            "sample": f"C port of DroneSwarmEnv.step (oracle/swarm_oracle.c), OpenMP {why}; "
+            "sample": f"C port of {'DronePhysicsEnv (point-mass restatement)' if physics else 'DroneSwarmEnv'}"
+                      f".step (oracle/swarm_oracle.c), OpenMP {why}; "
                       f"N={n} x E={e} envs (the benched workload), {steps} steps in {el:.2f} s, "
-                      f"auto-reset on, bit-exact with the reference fixtures"}
+                      f"auto-reset on, " + ("bit-identical to the GPU kernel (physics parity unpinned)" if physics
+                                            else "bit-exact with the reference fixtures")}
 
 
 def cpu_python_variants(n: int, e: int, seconds: float, procs: int | None = None) -> list[dict]:
@@ -262,7 +266,7 @@ def main(argv=None):
     raw = {"num_drones": n}
     if args.no_term:
         raw.update(collision_radius=0.0, obstacle_radius=0.0, goal_radius=0.0)
-    vec = VecSwarm(e, raw, device=dev, auto_reset=True, seed=0, env_offset=offset,
+    vec = VecSwarm(e, raw, device=dev, auto_reset=True, seed=0, env_offset=offset, dynamics=args.dynamics,
                    with_global_state=args.ctde, persistent=not args.no_persistent,
                    waves_per_simd=args.waves_per_simd, groups=args.groups)
     vec.reset()
@@ -464,7 +468,8 @@ def main(argv=None):
         value = total / wall_max
         bytes_launch = vec.algorithmic_bytes_per_step()
         achieved = bytes_launch / (kern_max * 1e-3) / 1e9
-        wl = f"kinematic+swarm N={n} E={e}{' noterm' if args.no_term else ''}" + \
+        wl = ("kinematic+swarm" if args.dynamics == "kinematic" else "physics") + \
+             f" N={n} E={e}{' noterm' if args.no_term else ''}" + \
              (" +global_state" if args.ctde else "")
         prof = profile_record(wl) or {}
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -505,8 +510,10 @@ def main(argv=None):
                               "note": "untimed replays after the W warm-up steps, before the timed region"},
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (device-RNG episodes, uniform(-1,1) actions)",
-            "config": {"workload": f"N={n} drones x E={e} envs per GPU, kinematic dynamics + "
-                                   f"swarm reward, in-kernel auto-reset"
+            "config": {"workload": f"N={n} drones x E={e} envs per GPU, "
+                                   + ("kinematic dynamics + swarm reward" if args.dynamics == "kinematic"
+                                      else "point-mass physics restatement (24 substeps) + physics reward")
+                                   + ", in-kernel auto-reset"
                                    f"{', no-termination radii' if args.no_term else ''}"
                                    f"{', CTDE global_state emitted' if args.ctde else ''}",
                        "baseline_config": args.label,
@@ -532,8 +539,8 @@ def main(argv=None):
                              "weights": "random-init TorchFC [256, 256] relu (no checkpoint)"}
             rec["roofline"]["note"] = "env-step roofline fields cover the whole rollout step"
         if not args.no_cpu_baseline and world == 1:
-            rec["cpu_baseline"] = cpu_baseline_port(n, e, args.cpu_seconds, raw)
-            if args.cpu_variant_seconds > 0 and not args.no_term:
+            rec["cpu_baseline"] = cpu_baseline_port(n, e, args.cpu_seconds, raw, args.dynamics == "physics")
+            if args.cpu_variant_seconds > 0 and not args.no_term and args.dynamics == "kinematic":
                 rec["cpu_baseline_variants"] = cpu_python_variants(n, e, args.cpu_variant_seconds)
         print(json.dumps(rec), flush=True)
     if world > 1:

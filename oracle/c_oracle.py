@@ -125,7 +125,7 @@ class Runner:
     """Persistent-buffer stepping of the C oracle (no per-call copies or allocations): the
     bench's CPU-baseline loop.  State arrays are updated in place by every call."""
 
-    def __init__(self, cfg: dict, num_envs: int, *, seed=0, env_offset=0, nthreads=0):
+    def __init__(self, cfg: dict, num_envs: int, *, seed=0, env_offset=0, nthreads=0, physics=False):
         self.cfg, self.e, self.seed, self.nthreads = cfg, int(num_envs), int(seed), int(nthreads)
         n, m = int(cfg["num_drones"]), int(cfg["num_obstacles"])
         d = 9 + 4 * max(int(cfg["neighbor_k"]), 0) + 4 * max(int(cfg["sensed_obstacles"]), 0)
@@ -139,7 +139,7 @@ class Runner:
                         env_done=np.zeros(e, np.uint8), dist_goal=np.zeros((e, n), np.float32),
                         flags=np.zeros((e, n), np.uint8),
                         global_state=np.zeros((e, 6 * n + 3), np.float32))
-        self.prm = make_params(cfg, e, auto_reset=True, seed=seed, env_offset=env_offset)
+        self.prm = make_params(cfg, e, physics=physics, auto_reset=True, seed=seed, env_offset=env_offset)
         self._call(1, None)  # device-RNG reset of every env
 
     def _call(self, mode: int, actions) -> None:
