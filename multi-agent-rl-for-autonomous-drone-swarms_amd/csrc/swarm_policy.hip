@@ -90,11 +90,24 @@ uint16_t bf16_rne(float f) {
 // ---------------------------------------------------------------- bf16 kernel
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 
+// 8 accumulator values -> bf16 fragment, relu'd after the conversion: round-to-nearest keeps the
+// sign, so relu(bf16(x)) == bf16(relu(x)), and a bf16 with the sign bit set is a negative int16:
+// one v_pk_max_i16 with 0 relus two values (an f32 relu costs a canonicalising v_max plus the max
+// on MFMA outputs: 4x the instructions).
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(2))) short s16x2;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 __device__ __forceinline__ bf16x8 pack8(const f32x16& a, int s, bool act) {
-  bf16x8 r;
+  u32x4 w;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (__bf16)(act ? relu(a[8 * s + j]) : a[8 * s + j]);
-  return r;
+  for (int q = 0; q < 4; ++q) {
+    const bf16x2 p = __builtin_convertvector((f32x2){a[8 * s + 2 * q], a[8 * s + 2 * q + 1]}, bf16x2);  // v_cvt_pk_bf16_f32
+    s16x2 v = __builtin_bit_cast(s16x2, p);
+    if (act) v = __builtin_elementwise_max(v, (s16x2){0, 0});  // v_pk_max_i16
+    w[q] = __builtin_bit_cast(unsigned, v);
+  }
+  return __builtin_bit_cast(bf16x8, w);
 }
 
 // Philox4x32-10 (same constants as the env's device reset)
@@ -120,143 +133,192 @@ struct FwdArgs {
   uint32_t seed_lo, seed_hi, ctr_lo, ctr_hi;
 };
 
-template <int WAVES, int MODE>
-__global__ void __launch_bounds__(64 * WAVES) policy_mlp_bf16(const FwdArgs A) {
+// T row tiles per wave (T = 2: every weight fragment read from LDS feeds two MFMAs, halving the
+// LDS bytes per FLOP — one 1-KB A fragment per 32x32x16 MFMA is the whole LDS bandwidth of a CU
+// at the MFMA peak; T = 2 needs ~330 registers, i.e. one wave per SIMD).
+// IN_C / OUT_C: compile-time obs / logits widths (0 = runtime): the obs gather's pad and bias
+// selects and the layer-3 row masks fold away for the env's default D = 37, out = 6.
+template <int WAVES, int MODE, int T, int IN_C = 0, int OUT_C = 0>
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVES / 4 > 0 ? WAVES / 4 : 1)))
+policy_mlp_bf16(const FwdArgs A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const Bf16Layout L(A.out);
-  {  // stage the packed weights in LDS (once per workgroup)
+  {  // stage the packed weights (~159 KB) in LDS, once per workgroup: 8 loads in flight per
+     // thread per round (a load-then-store loop pays one global round trip per 16 B x threads)
     const int4* src = reinterpret_cast<const int4*>(A.w);
     int4* dst = reinterpret_cast<int4*>(lds);
     const int n16 = (int)(L.total / 16);
-    for (int i = threadIdx.x; i < n16; i += 64 * WAVES) dst[i] = src[i];
+    constexpr int UNR = 8, STRIDE = 64 * WAVES;
+    for (int base = threadIdx.x; base < n16; base += STRIDE * UNR) {
+      int4 v[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int i = base + u * STRIDE;
+        v[u] = src[i < n16 ? i : n16 - 1];
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int i = base + u * STRIDE;
+        if (i < n16) dst[i] = v[u];
+      }
+    }
   }
   __syncthreads();
   const int wave = threadIdx.x >> 6;
   const long long ntiles = (A.rows + 31) / 32;
+  const long long ngroups = (ntiles + T - 1) / T;
   const float* b2 = reinterpret_cast<const float*>(lds + L.b2);
   const float* b3 = reinterpret_cast<const float*>(lds + L.b3);
-  for (long long tile = (long long)blockIdx.x * WAVES + wave; tile < ntiles; tile += (long long)gridDim.x * WAVES) {
-    // Opaque per tile: the lane index and the layer dims.  Everything derived from them (fragment
-    // addresses, the obs element offsets and their pad/bias selects, the layer-3 row masks) is
-    // recomputed per tile instead of being hoisted out of the loop, where it would stay live
-    // next to h1/h2 (64 + 64 VGPRs) and spill.
-    int lane = threadIdx.x & 63, in = A.in, out = A.out;
-    asm volatile("" : "+v"(lane), "+s"(in), "+s"(out));
-    const int n = lane & 31, h = lane >> 5;
+  for (long long grp = (long long)blockIdx.x * WAVES + wave; grp < ngroups; grp += (long long)gridDim.x * WAVES) {
+    // Opaque per tile group: the lane index and the layer dims.  Everything derived from them
+    // (fragment addresses, the obs element offsets and their pad/bias selects, the layer-3 row
+    // masks) is recomputed per group instead of being hoisted out of the loop, where it would
+    // stay live next to h1/h2 and spill.
+    int lane = threadIdx.x & 63, in_r = A.in, out_r = A.out;
+    asm volatile("" : "+v"(lane), "+s"(in_r), "+s"(out_r));
+    const int in = IN_C ? IN_C : in_r, out = OUT_C ? OUT_C : out_r;
+    const int n = lane & 31, h = (lane >> 5) & 1;  // h in [0, 1]: k-range facts fold the obs selects
     const bool w3lane = n < out;
     const int w3idx = h * out + n;
     const uint32_t lb = 16u * (uint32_t)lane;
     const bf16x8* w1f = reinterpret_cast<const bf16x8*>(lds + L.w1 + lb);
     const bf16x8* w2f = reinterpret_cast<const bf16x8*>(lds + L.w2 + lb);
     const bf16x8* w3f = reinterpret_cast<const bf16x8*>(lds + L.w3);
-    const long long row = tile * 32 + n;
-    const bool valid = row < A.rows;
+    long long row[T];
+    bool valid[T];
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+      row[u] = (grp * T + u) * 32 + n;
+      valid[u] = row[u] < A.rows;
+    }
     // ---- obs fragments (B of layer 1): x[row][16 ks + 8 h + j], x[in] = 1 (bias column).
     // Unconditional loads from clamped addresses (one wait for all of them), then selects.
-    const float* xr = A.obs + (valid ? row : A.rows - 1) * in;
-    float xv[KS1 * 8];
+    bf16x8 xb[T][KS1];
 #pragma unroll
-    for (int ks = 0; ks < KS1; ++ks)
+    for (int u = 0; u < T; ++u) {
+      const float* xr = A.obs + (valid[u] ? row[u] : A.rows - 1) * in;
+      float xv[KS1 * 8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 16 * ks + 8 * h + j;
-        xv[ks * 8 + j] = xr[k < in ? k : in - 1];
-      }
-    bf16x8 xb[KS1];
+      for (int ks = 0; ks < KS1; ++ks)
 #pragma unroll
-    for (int ks = 0; ks < KS1; ++ks)
+        for (int j = 0; j < 8; ++j) {
+          const int k = 16 * ks + 8 * h + j;
+          xv[ks * 8 + j] = xr[k < in ? k : in - 1];
+        }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 16 * ks + 8 * h + j;
-        xb[ks][j] = (__bf16)(k < in ? xv[ks * 8 + j] : (k == in ? 1.f : 0.f));
-      }
-    // ---- layer 1: 256 x (in + 1), relu -> h1 (16 k-step fragments)
-    bf16x8 h1[KS2];
+      for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 16 * ks + 8 * h + j;
+          xb[u][ks][j] = (__bf16)(k < in ? xv[ks * 8 + j] : (k == in ? 1.f : 0.f));
+        }
+    }
+    // ---- layer 1: 256 x (in + 1), relu -> h1 (16 k-step fragments per tile)
+    bf16x8 h1[T][KS2];
 #pragma unroll
     for (int ob = 0; ob < OB; ++ob) {
-      f32x16 acc = {};
+      f32x16 acc[T];
 #pragma unroll
-      for (int ks = 0; ks < KS1; ++ks) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[(ob * KS1 + ks) * 64], xb[ks], acc, 0, 0, 0);
-      h1[2 * ob] = pack8(acc, 0, true);
-      h1[2 * ob + 1] = pack8(acc, 1, true);
+      for (int u = 0; u < T; ++u) acc[u] = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks) {
+        const bf16x8 w = w1f[(ob * KS1 + ks) * 64];
+#pragma unroll
+        for (int u = 0; u < T; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w, xb[u][ks], acc[u], 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < T; ++u) {
+        h1[u][2 * ob] = pack8(acc[u], 0, true);
+        h1[u][2 * ob + 1] = pack8(acc[u], 1, true);
+      }
       __builtin_amdgcn_sched_barrier(0);  // keep each out block's fragment reads inside it
     }
-    // ---- layer 2: 256 x 256, relu -> h2
-    bf16x8 h2[KS2];
-#pragma unroll
-    for (int ob = 0; ob < OB; ++ob) {
-      f32x16 acc;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 b = *reinterpret_cast<const float4*>(b2 + ob * 32 + 8 * g + 4 * h);
-        acc[4 * g + 0] = b.x; acc[4 * g + 1] = b.y; acc[4 * g + 2] = b.z; acc[4 * g + 3] = b.w;
-      }
-#pragma unroll
-      for (int ks = 0; ks < KS2; ++ks) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2f[(ob * KS2 + ks) * 64], h1[ks], acc, 0, 0, 0);
-        if ((ks & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // <= 8 fragments (32 VGPRs) in flight
-      }
-      h2[2 * ob] = pack8(acc, 0, true);
-      h2[2 * ob + 1] = pack8(acc, 1, true);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // ---- layer 3: out x 256 (rows >= out are zero fragments)
-    f32x16 acc;
+    // ---- layer 2 (256 x 256, relu) fused with layer 3 (out x 256): each out block's two
+    // relu'd bf16 fragments are the B operands of layer 3's k-steps 2ob, 2ob+1 right away, so h2
+    // is never held whole (64 fewer VGPRs per tile)
+    f32x16 acc3[T];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
-      acc[i] = m < out ? b3[m] : 0.f;
+#pragma unroll
+      for (int u = 0; u < T; ++u) acc3[u][i] = m < out ? b3[m] : 0.f;
     }
 #pragma unroll
-    for (int ks = 0; ks < KS2; ++ks) {
-      bf16x8 a = {};
-      if (w3lane) a = w3f[ks * 2 * out + w3idx];
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, h2[ks], acc, 0, 0, 0);
-    }
-    // ---- outputs: lane holds logits m = (i&3) + 8(i>>2) + 4h of its row (out <= 12: i < 8)
-    if (A.logits && valid) {
+    for (int ob = 0; ob < OB; ++ob) {
+      f32x16 acc[T];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (m < out) A.logits[row * out + m] = acc[i];
-      }
-    }
-    if (A.actions) {
-      // gather the row's logits 0..out-1 on the lane pair (n, n + 32): half 0 holds m 0-3, 8-11;
-      // half 1 holds m 4-7
-      float lg[12];
+      for (int g = 0; g < 4; ++g) {
+        const float4 b = *reinterpret_cast<const float4*>(b2 + ob * 32 + 8 * g + 4 * h);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float mine = acc[i];
-        const float other = __shfl_xor(mine, 32);
-        const int m_me = (i & 3) + 8 * (i >> 2) + 4 * h, m_ot = (i & 3) + 8 * (i >> 2) + 4 * (1 - h);
-        if (m_me < 12) lg[m_me] = mine;
-        if (m_ot < 12) lg[m_ot] = other;
-      }
-      const int ad = out / 2;
-      if (h == 0 && valid) {
-        float z[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if constexpr (MODE == SWARM_POLICY_ACT_SAMPLE) {  // Box-Muller normals from Philox(seed; row, counter)
-          uint32_t c[4] = {(uint32_t)row, (uint32_t)((unsigned long long)row >> 32), A.ctr_lo, A.ctr_hi};
-          philox(c, A.seed_lo, A.seed_hi);
-          uint32_t c2[4] = {(uint32_t)row, (uint32_t)((unsigned long long)row >> 32) ^ 0x80000000u, A.ctr_lo, A.ctr_hi};
-          if (ad > 2) philox(c2, A.seed_lo, A.seed_hi);
-          const uint32_t u[8] = {c[0], c[1], c[2], c[3], c2[0], c2[1], c2[2], c2[3]};
-#pragma unroll
-          for (int p = 0; p < 3; ++p) {
-            const float u1 = ((float)(u[2 * p] >> 8) + 0.5f) * 0x1p-24f;
-            const float u2 = (float)(u[2 * p + 1] >> 8) * 0x1p-24f;
-            const float r = sqrtf(-2.f * logf(u1));
-            z[2 * p] = r * cosf(6.28318530717958647692f * u2);
-            z[2 * p + 1] = r * sinf(6.28318530717958647692f * u2);
-          }
+        for (int u = 0; u < T; ++u) {
+          acc[u][4 * g + 0] = b.x; acc[u][4 * g + 1] = b.y; acc[u][4 * g + 2] = b.z; acc[u][4 * g + 3] = b.w;
         }
+      }
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
-          if (k < ad) {
-            float a = lg[k];
-            if constexpr (MODE == SWARM_POLICY_ACT_SAMPLE) a = a + expf(lg[ad + k]) * z[k];
-            A.actions[row * ad + k] = a;
+      for (int ks = 0; ks < KS2; ++ks) {
+        const bf16x8 w = w2f[(ob * KS2 + ks) * 64];
+#pragma unroll
+        for (int u = 0; u < T; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w, h1[u][ks], acc[u], 0, 0, 0);
+        if ((ks & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // <= 8 fragments (32 VGPRs) in flight
+      }
+      bf16x8 a0 = {}, a1 = {};
+      if (w3lane) {
+        a0 = w3f[(2 * ob) * 2 * out + w3idx];
+        a1 = w3f[(2 * ob + 1) * 2 * out + w3idx];
+      }
+#pragma unroll
+      for (int u = 0; u < T; ++u) {
+        acc3[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, pack8(acc[u], 0, true), acc3[u], 0, 0, 0);
+        acc3[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, pack8(acc[u], 1, true), acc3[u], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+      // ---- outputs: lane holds logits m = (i&3) + 8(i>>2) + 4h of its row (out <= 12: i < 8)
+      if (A.logits && valid[u]) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (m < out) A.logits[row[u] * out + m] = acc3[u][i];
+        }
+      }
+      if (A.actions) {
+        // gather the row's logits 0..11 on the writing lane (half h = 0): it holds m 0-3 and
+        // 8-11, its partner n + 32 holds m 4-7 (static indices: no per-element selects)
+        float lg[12];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          lg[i] = acc3[u][i];
+          lg[4 + i] = __shfl_xor(acc3[u][i], 32);
+          lg[8 + i] = acc3[u][4 + i];
+        }
+        const int ad = out / 2;
+        if (h == 0 && valid[u]) {
+          float z[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          if constexpr (MODE == SWARM_POLICY_ACT_SAMPLE) {  // Box-Muller normals from Philox(seed; row, counter)
+            const long long r = row[u];
+            uint32_t c[4] = {(uint32_t)r, (uint32_t)((unsigned long long)r >> 32), A.ctr_lo, A.ctr_hi};
+            philox(c, A.seed_lo, A.seed_hi);
+            uint32_t c2[4] = {(uint32_t)r, (uint32_t)((unsigned long long)r >> 32) ^ 0x80000000u, A.ctr_lo, A.ctr_hi};
+            if (ad > 2) philox(c2, A.seed_lo, A.seed_hi);
+            const uint32_t uu[8] = {c[0], c[1], c[2], c[3], c2[0], c2[1], c2[2], c2[3]};
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+              const float u1 = ((float)(uu[2 * p] >> 8) + 0.5f) * 0x1p-24f;
+              const float u2 = (float)(uu[2 * p + 1] >> 8) * 0x1p-24f;
+              const float rr = sqrtf(-2.f * logf(u1));
+              z[2 * p] = rr * cosf(6.28318530717958647692f * u2);
+              z[2 * p + 1] = rr * sinf(6.28318530717958647692f * u2);
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            if (k < ad) {
+              float a = lg[k];
+              if constexpr (MODE == SWARM_POLICY_ACT_SAMPLE) a = a + expf(lg[ad + k]) * z[k];
+              A.actions[row[u] * ad + k] = a;
+            }
           }
         }
       }
@@ -348,7 +410,15 @@ __global__ void __launch_bounds__(64 * WAVES) policy_mlp_f32(const FwdArgs A) {
   }
 }
 
-constexpr int BF16_WAVES = 8;
+#ifndef SWARM_POLICY_WAVES
+#define SWARM_POLICY_WAVES 8
+#endif
+constexpr int BF16_WAVES = SWARM_POLICY_WAVES;  // T = 1: waves per workgroup (one workgroup per CU: the LDS blob)
+#ifndef SWARM_POLICY_TILES
+#define SWARM_POLICY_TILES 1
+#endif
+constexpr int BF16_TILES = SWARM_POLICY_TILES;            // row tiles per wave
+constexpr int BF16_WAVES_T = BF16_TILES > 1 ? 4 : BF16_WAVES;  // T = 2: one wave per SIMD
 constexpr int F32_WAVES = 4;
 
 thread_local char g_perr[256] = "";
@@ -467,13 +537,17 @@ int swarm_policy_forward(const swarm_policy_t* p, const float* obs, long long ro
   hipStream_t s = (hipStream_t)hip_stream;
   if (p->precision == SWARM_POLICY_BF16) {
     const int lds = (int)Bf16Layout(p->out_dim).total;
-    auto fn = action_mode == SWARM_POLICY_ACT_SAMPLE ? policy_mlp_bf16<BF16_WAVES, SWARM_POLICY_ACT_SAMPLE>
-                                                     : policy_mlp_bf16<BF16_WAVES, SWARM_POLICY_ACT_MEAN>;
+    const bool dflt = p->in_dim == 37 && p->out_dim == 6;  // K = 3, Ms = 4 obs; 3-d Gaussian actions
+    auto fn = action_mode == SWARM_POLICY_ACT_SAMPLE
+                  ? (dflt ? policy_mlp_bf16<BF16_WAVES_T, SWARM_POLICY_ACT_SAMPLE, BF16_TILES, 37, 6>
+                          : policy_mlp_bf16<BF16_WAVES_T, SWARM_POLICY_ACT_SAMPLE, BF16_TILES>)
+                  : (dflt ? policy_mlp_bf16<BF16_WAVES_T, SWARM_POLICY_ACT_MEAN, BF16_TILES, 37, 6>
+                          : policy_mlp_bf16<BF16_WAVES_T, SWARM_POLICY_ACT_MEAN, BF16_TILES>);
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
         hipSuccess)
       return pfail(SWARM_EHIP, "hipFuncSetAttribute failed");
-    const int grid = grid_for(BF16_WAVES, (rows + 31) / 32);
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * BF16_WAVES), lds, s, a);
+    const int grid = grid_for(BF16_WAVES_T, ((rows + 31) / 32 + BF16_TILES - 1) / BF16_TILES);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * BF16_WAVES_T), lds, s, a);
   } else {
     const int grid = grid_for(F32_WAVES, (rows + 15) / 16) * 2;
     hipLaunchKernelGGL(policy_mlp_f32<F32_WAVES>, dim3(grid), dim3(64 * F32_WAVES), 0, s, a);
