@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SWARM_ABI_VERSION 3
+#define SWARM_ABI_VERSION 4
 
 /* error codes */
 #define SWARM_OK 0
@@ -131,7 +131,52 @@ typedef struct swarm_state {
   uint32_t* work;      /* [SWARM_WORK_WORDS] env-queue heads of the persistent swarm_step64: zeroed
                           once by the caller, left zeroed by every call; NULL = one workgroup per
                           env.  Belongs to this state: concurrent calls need distinct buffers. */
+  struct swarm_env_cfg* env_cfg;             /* [E] per-env parameters (NULL: every env uses
+                                                swarm_params_t); see swarm_env_cfg_set */
+  const struct swarm_env_cfg* env_cfg_next;  /* [E] parameters of each env's NEXT episode: a reset
+                                                (auto or swarm_reset) copies it into env_cfg before
+                                                drawing.  NULL: episodes keep env_cfg.  Needs env_cfg. */
 } swarm_state_t;
+
+/*
+ * Per-env parameters (curriculum stages configs/curriculum_v1.yaml:9-60 and
+ * domain randomisation configs/domain_randomization_v1.yaml:9-57 as per-env tensors).  One 64-B
+ * record per env, derived on the device by swarm_env_cfg_set from per-env values exactly as the
+ * library derives the uniform constants from swarm_params_t, so that an env with record r behaves
+ * bit-for-bit like a launch whose swarm_params_t carries r's values.  N, K, Ms, rewards and radii
+ * other than the obstacle radius stay uniform (they fix the tensor shapes or are not randomised).
+ * With env_cfg set, swarm_step launches the generic kernel (the step64 specialisation assumes
+ * uniform parameters).
+ */
+typedef struct swarm_env_cfg {
+  float half_w;          /* (float)(world_size / 2)  world clip and reset draw bounds */
+  float neg_half_w;      /* (float)(-world_size / 2) */
+  float width_w;         /* (float)world_size */
+  float dt;              /* kinematic integrator step (physics: substeps stay uniform) */
+  float max_speed;
+  float max_accel;
+  float s_vmax;          /* largest s with sqrtf(s) <= (float)max_speed */
+  float s_obst;          /* same for (float)(collision_radius + obstacle_radius) */
+  float s_phys_obst;     /* same for (float)(obstacle_radius + drone_contact_radius) */
+  int32_t max_steps;
+  int32_t num_obstacles; /* active obstacles, 0..swarm_params_t.num_obstacles (the state keeps M
+                            slots; slots >= num_obstacles are zero and ignored) */
+  int32_t reserved;
+  double max_speed_d;    /* max_speed as given (physics observation clamp) */
+  double world_size;     /* as given (for readers) */
+} swarm_env_cfg_t;
+
+/* Per-env values for swarm_env_cfg_set: each pointer is a device array [E] or NULL (= the
+ * swarm_params_t value for every env). */
+typedef struct swarm_env_overrides {
+  const double* world_size;
+  const double* dt;
+  const double* max_speed;
+  const double* max_accel;
+  const double* obstacle_radius;
+  const int32_t* max_steps;
+  const int32_t* num_obstacles;  /* clamped to [0, swarm_params_t.num_obstacles] */
+} swarm_env_overrides_t;
 
 #define SWARM_WORK_WORDS 256  /* 8 dequeue heads (one per XCD), one 128-B line each */
 
@@ -279,6 +324,15 @@ int swarm_eval_begin(const swarm_params_t* p, const swarm_eval_t* ev, const swar
 int swarm_eval_update(const swarm_params_t* p, const swarm_eval_t* ev, const swarm_out_t* out, void* hip_stream);
 
 const char* swarm_eval_last_error(void);
+
+/*
+ * Write the per-env parameter records cfg[e] (device, [E] swarm_env_cfg_t) of the masked envs
+ * (env_mask NULL = all) from `ov` and the uniform fields of `p`.  Async on hip_stream.  Point
+ * swarm_state_t.env_cfg (the current episode) or .env_cfg_next (the next episode, e.g. a domain
+ * randomisation draw made after the step that reset the env) at the result.
+ */
+int swarm_env_cfg_set(const swarm_params_t* p, const swarm_env_overrides_t* ov, const uint8_t* env_mask,
+                      swarm_env_cfg_t* cfg, void* hip_stream);
 
 #ifdef __cplusplus
 }

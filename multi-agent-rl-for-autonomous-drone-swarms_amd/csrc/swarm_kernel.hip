@@ -113,6 +113,28 @@ struct KParams {
   double goal_radius, kp, r_goal, r_col, kf, vmax_d;
 };
 
+// The launch-uniform parameters as a per-env record (swarm_env_cfg_t: what swarm_env_cfg_set
+// derives from the same values, field for field).
+__device__ __forceinline__ swarm_env_cfg_t uniform_env_cfg(const KParams& P) {
+  swarm_env_cfg_t c;
+  c.half_w = P.half_w;
+  c.neg_half_w = P.neg_half_w;
+  c.width_w = P.width_w;
+  c.dt = P.dt;
+  c.max_speed = P.vmax;
+  c.max_accel = P.amax;
+  c.s_vmax = P.s_vmax;
+  c.s_obst = P.s_obst;
+  c.s_phys_obst = P.s_phys_obst;
+  c.max_steps = P.max_steps;
+  c.num_obstacles = P.M;
+  c.reserved = 0;
+  c.max_speed_d = P.vmax_d;
+  c.world_size = 0.0;
+  return c;
+}
+__device__ __forceinline__ int clamp_obstacles(int m, int M) { return m < 0 ? 0 : (m > M ? M : m); }
+
 // ------------------------------------------------------------------ exact numerics
 // Correctly rounded square roots.  NB: HIP's __fsqrt_rn is v_sqrt_f32 (1 ulp) unless
 // OCML_BASIC_ROUNDED_OPERATIONS is defined; llvm.sqrt lowers to the IEEE-exact sequence.
@@ -638,6 +660,12 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   const long long env0 = (long long)blockIdx.x * G;
   const long long env = env0 + team;
   const bool env_ok = env < P.E;
+  // this env's parameters: its swarm_env_cfg_t record (per-env curriculum / randomisation) or
+  // the launch-uniform values
+  swarm_env_cfg_t C;
+  if (S.env_cfg != nullptr && env_ok) C = S.env_cfg[env];
+  else C = uniform_env_cfg(P);
+  int Me = clamp_obstacles(C.num_obstacles, M);  // active obstacles (slots >= Me are ignored)
   const bool is_agent = env_ok && t < N;
   float4* ring = reinterpret_cast<float4*>(smem) + team * P.ring;
   float4* obst4 = reinterpret_cast<float4*>(smem + P.off_obst) + team * P.obst_stride;
@@ -658,7 +686,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   int stepc = 0;
   float gx = 0.f, gy = 0.f, gz = 0.f;
   if (env_ok) {
-    for (int m = t; m < M; m += L) {
+    for (int m = t; m < Me; m += L) {
       const float* o = S.obstacles + (env * M + m) * 3;
       obst4[m] = make_float4(o[0], o[1], o[2], 0.f);
     }
@@ -700,45 +728,45 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       if (act) {  // drone_swarm_env.py:98-111
         prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
         if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
-        ax = clampf(ax, -1.f, 1.f) * P.amax;
-        ay = clampf(ay, -1.f, 1.f) * P.amax;
-        az = clampf(az, -1.f, 1.f) * P.amax;
-        vx = vx + ax * P.dt;
-        vy = vy + ay * P.dt;
-        vz = vz + az * P.dt;
+        ax = clampf(ax, -1.f, 1.f) * C.max_accel;
+        ay = clampf(ay, -1.f, 1.f) * C.max_accel;
+        az = clampf(az, -1.f, 1.f) * C.max_accel;
+        vx = vx + ax * C.dt;
+        vy = vy + ay * C.dt;
+        vz = vz + az * C.dt;
         const float s_sp = sqsum_1d(vx, vy, vz);  // _clip_speed :179-183
-        if (!(s_sp <= P.s_vmax)) {
+        if (!(s_sp <= C.s_vmax)) {
           const float sp = sqrt_rn(s_sp);
-          if (!(sp <= P.vmax || sp < (float)1e-8)) {
-            vx = (vx / sp) * P.vmax;
-            vy = (vy / sp) * P.vmax;
-            vz = (vz / sp) * P.vmax;
+          if (!(sp <= C.max_speed || sp < (float)1e-8)) {
+            vx = (vx / sp) * C.max_speed;
+            vy = (vy / sp) * C.max_speed;
+            vz = (vz / sp) * C.max_speed;
           }
         }
-        px = px + vx * P.dt;
-        py = py + vy * P.dt;
-        pz = pz + vz * P.dt;
+        px = px + vx * C.dt;
+        py = py + vy * C.dt;
+        pz = pz + vz * C.dt;
       }
       if (n_active > 0) {  // world clip of ALL drones, :113-117
-        px = clampf(px, P.neg_half_w, P.half_w);
-        py = clampf(py, P.neg_half_w, P.half_w);
-        pz = clampf(pz, P.neg_half_w, P.half_w);
+        px = clampf(px, C.neg_half_w, C.half_w);
+        py = clampf(py, C.neg_half_w, C.half_w);
+        pz = clampf(pz, C.neg_half_w, C.half_w);
       }
     } else {
       // point-mass restatement of drone_physics_env.py:323-360
       const float h = P.h;
-      const float cx = has ? ax * P.amax : 0.f;
-      const float cy = has ? ay * P.amax : 0.f;
-      float cz = has ? az * P.amax + P.gcomp : 0.f;
+      const float cx = has ? ax * C.max_accel : 0.f;
+      const float cy = has ? ay * C.max_accel : 0.f;
+      float cz = has ? az * C.max_accel + P.gcomp : 0.f;
       cz = cz + P.g;
       float fac = 1.f;
       if (P.damping_law == 1) fac = (float)pow((double)(1.f - damp), (double)h);
       for (int s = 0; s < P.substeps; ++s) {
         const float sp = sqrt_rn(sqsum_1d(vx, vy, vz));
-        if (has && sp > P.vmax) {
-          vx = (vx / sp) * P.vmax;
-          vy = (vy / sp) * P.vmax;
-          vz = (vz / sp) * P.vmax;
+        if (has && sp > C.max_speed) {
+          vx = (vx / sp) * C.max_speed;
+          vy = (vy / sp) * C.max_speed;
+          vz = (vz / sp) * C.max_speed;
         }
         if (P.damping_law == 0) {
           const float sp2 = sqrt_rn(sqsum_1d(vx, vy, vz));
@@ -759,12 +787,16 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   }
 
   auto draw_env = [&]() {  // new episode for this team (drone_swarm_env.py:72-80 ranges)
+    if (S.env_cfg_next != nullptr) {  // the next episode's parameters take over
+      C = S.env_cfg_next[env];
+      Me = clamp_obstacles(C.num_obstacles, M);
+    }
     uint32_t w[4];
     if (t < N) {
       draw_block(P, genv, episode_new, (uint32_t)t, w);
-      px = uni(w[0], P.neg_half_w, P.width_w);
-      py = uni(w[1], P.neg_half_w, P.width_w);
-      pz = uni(w[2], P.neg_half_w, P.width_w);
+      px = uni(w[0], C.neg_half_w, C.width_w);
+      py = uni(w[1], C.neg_half_w, C.width_w);
+      pz = uni(w[2], C.neg_half_w, C.width_w);
       vx = vy = vz = 0.f;
       act = true;
       if constexpr (DYN == DYN_PHYS) {
@@ -773,15 +805,19 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       }
     }
     for (int m = t; m < M; m += L) {
+      if (m >= Me) {  // inactive slot of a per-env obstacle count: stored as zeros
+        obst4[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+        continue;
+      }
       draw_block(P, genv, episode_new, (uint32_t)(N + m), w);
-      float oz = uni(w[2], P.neg_half_w, P.width_w);
+      float oz = uni(w[2], C.neg_half_w, C.width_w);
       if constexpr (DYN == DYN_PHYS) oz = fmaxf(oz, 0.5f);
-      obst4[m] = make_float4(uni(w[0], P.neg_half_w, P.width_w), uni(w[1], P.neg_half_w, P.width_w), oz, 0.f);
+      obst4[m] = make_float4(uni(w[0], C.neg_half_w, C.width_w), uni(w[1], C.neg_half_w, C.width_w), oz, 0.f);
     }
-    draw_block(P, genv, episode_new, (uint32_t)(N + M), w);
-    gx = uni(w[0], P.neg_half_w, P.width_w);
-    gy = uni(w[1], P.neg_half_w, P.width_w);
-    gz = uni(w[2], P.neg_half_w, P.width_w);
+    draw_block(P, genv, episode_new, (uint32_t)(N + Me), w);
+    gx = uni(w[0], C.neg_half_w, C.width_w);
+    gy = uni(w[1], C.neg_half_w, C.width_w);
+    gz = uni(w[2], C.neg_half_w, C.width_w);
     if constexpr (DYN == DYN_PHYS) gz = uni(w[3], 0.5f, 1.5f);
   };
   auto put_ring = [&](float w) {
@@ -845,8 +881,8 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         }
       }
       if constexpr (SWARM_ABLATE & ABL_OBST) {}
-      else if constexpr (DYN == DYN_KIN) obstacle_pass<MSL, true>(obst4, M, px, py, pz, act, P.s_obst, P.ob_keep, ok, ocoll);
-      else obstacle_pass<MSL, true>(obst4, M, px, py, pz, true, P.s_phys_obst, P.ob_keep, ok, ocoll);
+      else if constexpr (DYN == DYN_KIN) obstacle_pass<MSL, true>(obst4, Me, px, py, pz, act, C.s_obst, P.ob_keep, ok, ocoll);
+      else obstacle_pass<MSL, true>(obst4, Me, px, py, pz, true, C.s_phys_obst, P.ob_keep, ok, ocoll);
     } else {
       if constexpr (WAVE) {
         if constexpr (W64 && !(SWARM_ABLATE & ABL_W64)) pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
@@ -855,7 +891,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         if (blk_rot) pair_pass_block_fast<KS, 0>(pair_ring, N, t, px, py, pz, P.nb_keep, 0.f, nk, fsum, smin);
         else pair_pass_block<KS, 0>(ring, N, t, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
       }
-      obstacle_pass<MSL, false>(obst4, M, px, py, pz, false, 0.f, P.ob_keep, ok, ocoll);
+      obstacle_pass<MSL, false>(obst4, Me, px, py, pz, false, 0.f, P.ob_keep, ok, ocoll);
     }
   }
 
@@ -870,19 +906,19 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   // neighbour keys carry the rotation offset (wave teams, block rotation passes: `rot`) or the
   // drone index (block pair_pass_block)
   const int Kq = K;
-  const int Mse = Ms < M ? Ms : M;
   auto select_topk = [&](bool run, bool dkey, bool rot) {
+    const int Mse = Ms < Me ? Ms : Me;
     bool slow_nb = false, slow_ob = false;
     if (run && !(SWARM_ABLATE & ABL_FINISH)) {
       const int imod = rot ? (L - 1) : 0x7fffffff;
       if constexpr (KS > 0) slow_nb = !finish_keys<KS, false, true>(nk, ring, N, rot ? t : 0, imod, Kq, P.nb_keep, dkey, px, py, pz, wd, wj);
-      if constexpr (MSL > 0) slow_ob = !finish_keys<MSL, true, false>(ok, obst4, M, 0, 0x7fffffff, Mse, P.ob_keep, false, px, py, pz, od, oj);
+      if constexpr (MSL > 0) slow_ob = !finish_keys<MSL, true, false>(ok, obst4, Me, 0, 0x7fffffff, Mse, P.ob_keep, false, px, py, pz, od, oj);
     }
     if constexpr (KS > 0) {
       if (slow_nb) exact_select<NW, false>(ring, N, t, Kq, max_first(wd, Kq), px, py, pz, wd, wj);
     }
     if constexpr (MSL > 0) {
-      if (slow_ob) exact_select<OW, true>(obst4, M, -1, Mse, max_first(od, Mse), px, py, pz, od, oj);
+      if (slow_ob) exact_select<OW, true>(obst4, Me, -1, Mse, max_first(od, Mse), px, py, pz, od, oj);
     }
   };
   // the step's kinematic pass ranks by d~, every other pass by s'.  A step runs the finish only
@@ -964,7 +1000,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         term_all = true;
       } else {
         new_step = stepc + 1;
-        const bool tl = new_step >= P.max_steps;
+        const bool tl = new_step >= C.max_steps;
         const bool all_reached = !any_cand && !any_c && !tl;
         term_all = all_reached || any_c;
         trunc_all = tl && !term_all;
@@ -977,7 +1013,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       }
     } else {
       new_step = stepc + 1;
-      const bool tl = new_step >= P.max_steps;
+      const bool tl = new_step >= C.max_steps;
       const bool all_goals = !any_notall;
       const bool done = any_c || all_goals || tl;
       trunc_all = done && tl && !any_c && !all_goals;
@@ -1042,7 +1078,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         } else {
           pair_pass_block<KS, 0>(ring, N, t, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
         }
-        obstacle_pass<MSL, false>(obst4, M, px, py, pz, false, 0.f, P.ob_keep, ok, c2);
+        obstacle_pass<MSL, false>(obst4, Me, px, py, pz, false, 0.f, P.ob_keep, ok, c2);
       }
       select_topk(do_reset && is_agent, false, WAVE || blk_rot);
     }
@@ -1096,6 +1132,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     if (mode == MODE_STEP) S.step_count[env] = do_reset ? 0 : new_step;
     else if (mode == MODE_RESET && sel) S.step_count[env] = 0;
     if (new_episode) {
+      if (S.env_cfg_next != nullptr) S.env_cfg[env] = C;
       S.episode[env] = episode_new;
       S.goal[env * 3 + 0] = gx; S.goal[env * 3 + 1] = gy; S.goal[env * 3 + 2] = gz;
     }
@@ -1114,10 +1151,10 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   if constexpr (DYN == DYN_PHYS) {
     const double dvx = (double)vx, dvy = (double)vy, dvz = (double)vz;
     const double nv = dsqrt_rn(((dvx * dvx) + (dvy * dvy)) + (dvz * dvz));
-    if (nv > P.vmax_d) {
-      ovx = (float)((dvx / nv) * P.vmax_d);
-      ovy = (float)((dvy / nv) * P.vmax_d);
-      ovz = (float)((dvz / nv) * P.vmax_d);
+    if (nv > C.max_speed_d) {
+      ovx = (float)((dvx / nv) * C.max_speed_d);
+      ovy = (float)((dvy / nv) * C.max_speed_d);
+      ovz = (float)((dvz / nv) * C.max_speed_d);
     }
   }
 
@@ -1151,7 +1188,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         for (int u = 0; u < MSL - 1; ++u)
           if (u == s) { m = oj[u]; d = od[u]; }
       }
-      if (m < M) {
+      if (m < Me) {
         const float4 q = obst4[m];
         f0 = q.x - px; f1 = q.y - py; f2 = q.z - pz; f3 = d;
       }
@@ -2217,6 +2254,7 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
     return fail(SWARM_ENULL, "state buffer is NULL (pos/vel/goal/active/step_count/episode required)");
   if (kp.M > 0 && !s->obstacles) return fail(SWARM_ENULL, "state.obstacles is NULL with num_obstacles > 0");
   if (p->dynamics == DYN_PHYS && !s->damping) return fail(SWARM_ENULL, "state.damping is NULL in physics mode");
+  if (s->env_cfg_next && !s->env_cfg) return fail(SWARM_ENULL, "state.env_cfg_next needs state.env_cfg");
   if (!o->obs) return fail(SWARM_ENULL, "out.obs is NULL");
   if (mode == MODE_STEP) {
     if (!actions) return fail(SWARM_ENULL, "actions is NULL");
@@ -2227,7 +2265,7 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   // ballot-packed byte outputs need N == 64 and dword-aligned bool tensors
   kp.pack_bytes = (kp.N == 64 && mode == MODE_STEP && ((uintptr_t)o->terminated | (uintptr_t)o->truncated |
                                                        (uintptr_t)s->active) % 4 == 0) ? 1 : 0;
-  if (mode == MODE_STEP && step64_applies(p, kp) && kp.obs_vec4 && kp.pack_bytes) {
+  if (mode == MODE_STEP && step64_applies(p, kp) && kp.obs_vec4 && kp.pack_bytes && !s->env_cfg) {
     swarm_state_t st = *s;
     const int grid = step64_grid(p, kp.E);
     if (grid >= kp.E) st.work = nullptr;  // one env per workgroup: nothing to dequeue
@@ -2261,6 +2299,57 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
   return SWARM_OK;
+}
+
+// ---- per-env parameter records (swarm_env_cfg_set)
+// s_threshold on the device: the same search with IEEE sqrt (llvm.sqrt) and one-ulp steps on
+// the bit pattern (every argument here is finite and >= 0, so the patterns are ordered).
+__device__ float s_threshold_dev(float T) {
+  if (!(T >= 0.0f)) return -1.0f;
+  if (__builtin_isinf(T)) return __builtin_inff();
+  float s = T * T;
+  while (s > 0.0f && __builtin_sqrtf(s) > T) s = __uint_as_float(__float_as_uint(s) - 1u);
+  for (;;) {
+    const float nx = __uint_as_float(__float_as_uint(s) + 1u);
+    if (__builtin_isinf(nx) || __builtin_sqrtf(nx) > T) break;
+    s = nx;
+  }
+  return s;
+}
+
+struct EnvCfgBase {
+  int E, M, max_steps;
+  double world_size, dt, max_speed, max_accel, obstacle_radius, collision_radius, drone_contact_radius;
+};
+
+// one thread per env; the derivations are build_kparams' (double -> float conversions included)
+__global__ void __launch_bounds__(256) env_cfg_set_kernel(const EnvCfgBase B, const swarm_env_overrides_t ov,
+                                                          const uint8_t* __restrict__ env_mask,
+                                                          swarm_env_cfg_t* __restrict__ out) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B.E) return;
+  if (env_mask != nullptr && env_mask[e] == 0) return;
+  const double ws = ov.world_size ? ov.world_size[e] : B.world_size;
+  const double dt = ov.dt ? ov.dt[e] : B.dt;
+  const double vmax = ov.max_speed ? ov.max_speed[e] : B.max_speed;
+  const double amax = ov.max_accel ? ov.max_accel[e] : B.max_accel;
+  const double orad = ov.obstacle_radius ? ov.obstacle_radius[e] : B.obstacle_radius;
+  swarm_env_cfg_t c;
+  c.half_w = (float)(ws / 2.0);
+  c.neg_half_w = (float)(-ws / 2.0);
+  c.width_w = (float)ws;
+  c.dt = (float)dt;
+  c.max_speed = (float)vmax;
+  c.max_accel = (float)amax;
+  c.s_vmax = s_threshold_dev(c.max_speed);
+  c.s_obst = s_threshold_dev((float)(B.collision_radius + orad));
+  c.s_phys_obst = s_threshold_dev((float)(orad + B.drone_contact_radius));
+  c.max_steps = ov.max_steps ? ov.max_steps[e] : B.max_steps;
+  c.num_obstacles = clamp_obstacles(ov.num_obstacles ? ov.num_obstacles[e] : B.M, B.M);
+  c.reserved = 0;
+  c.max_speed_d = vmax;
+  c.world_size = ws;
+  out[e] = c;
 }
 
 }  // namespace
@@ -2357,6 +2446,32 @@ int swarm_reset(const swarm_params_t* p, const swarm_state_t* s, const uint8_t* 
 int swarm_observe(const swarm_params_t* p, const swarm_state_t* s, const uint8_t* env_mask, const swarm_out_t* o,
                   void* hip_stream) {
   return launch(MODE_OBSERVE, p, s, nullptr, nullptr, env_mask, o, hip_stream);
+}
+
+int swarm_env_cfg_set(const swarm_params_t* p, const swarm_env_overrides_t* ov, const uint8_t* env_mask,
+                      swarm_env_cfg_t* cfg, void* hip_stream) {
+  KParams kp;
+  const int rc = build_kparams(p, &kp, nullptr);
+  if (rc) return rc;
+  if (!ov) return fail(SWARM_ENULL, "overrides is NULL");
+  if (kp.E == 0) return SWARM_OK;
+  if (!cfg) return fail(SWARM_ENULL, "env_cfg is NULL");
+  EnvCfgBase b;
+  b.E = kp.E;
+  b.M = kp.M;
+  b.max_steps = p->max_steps;
+  b.world_size = p->world_size;
+  b.dt = p->dt;
+  b.max_speed = p->max_speed;
+  b.max_accel = p->max_accel;
+  b.obstacle_radius = p->obstacle_radius;
+  b.collision_radius = p->collision_radius;
+  b.drone_contact_radius = p->drone_contact_radius;
+  hipLaunchKernelGGL(env_cfg_set_kernel, dim3((kp.E + 255) / 256), dim3(256), 0, (hipStream_t)hip_stream, b, *ov,
+                     env_mask, cfg);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
+  return SWARM_OK;
 }
 
 }  // extern "C"

@@ -14,7 +14,7 @@ LIB_NAME = "libswarm_mi355x.so"
 LIB_DIR = Path(__file__).resolve().parent / "_lib"
 LIB_PATH = LIB_DIR / LIB_NAME
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 WORK_WORDS = 256  # SWARM_WORK_WORDS: u32 env-queue heads of the persistent swarm_step64
 
 PATH_AUTO = 0
@@ -59,8 +59,9 @@ EXPORTED_SYMBOLS = (
     "swarm_abi_version", "swarm_last_error", "swarm_params_default", "swarm_obs_dim",
     "swarm_query_launch", "swarm_step", "swarm_reset", "swarm_observe",
     "swarm_policy_packed_bytes", "swarm_policy_pack", "swarm_policy_forward", "swarm_policy_last_error",
-    "swarm_eval_begin", "swarm_eval_update", "swarm_eval_last_error",
+    "swarm_eval_begin", "swarm_eval_update", "swarm_eval_last_error", "swarm_env_cfg_set",
 )
+ENV_CFG_BYTES = 64  # sizeof(swarm_env_cfg_t)
 
 
 class NativeLibraryError(RuntimeError):
@@ -108,7 +109,24 @@ class SwarmParams(ctypes.Structure):
 class SwarmState(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name in
                 ("pos", "vel", "goal", "obstacles", "active", "step_count", "episode", "damping",
-                 "work")]
+                 "work", "env_cfg", "env_cfg_next")]
+
+
+class SwarmEnvCfg(ctypes.Structure):
+    """swarm_env_cfg_t: one env's derived parameters (64 B)."""
+    _fields_ = [(name, ctypes.c_float) for name in
+                ("half_w", "neg_half_w", "width_w", "dt", "max_speed", "max_accel", "s_vmax", "s_obst",
+                 "s_phys_obst")] + [("max_steps", ctypes.c_int32), ("num_obstacles", ctypes.c_int32),
+                                    ("reserved", ctypes.c_int32), ("max_speed_d", ctypes.c_double),
+                                    ("world_size", ctypes.c_double)]
+
+
+ENV_OVERRIDE_FIELDS = ("world_size", "dt", "max_speed", "max_accel", "obstacle_radius", "max_steps",
+                       "num_obstacles")
+
+
+class SwarmEnvOverrides(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name in ENV_OVERRIDE_FIELDS]
 
 
 class SwarmOut(ctypes.Structure):
@@ -185,6 +203,8 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.swarm_eval_update.argtypes = [P, ev, O, vp]
     lib.swarm_eval_last_error.restype = ctypes.c_char_p
     lib.swarm_eval_last_error.argtypes = []
+    lib.swarm_env_cfg_set.restype = ctypes.c_int
+    lib.swarm_env_cfg_set.argtypes = [P, ctypes.POINTER(SwarmEnvOverrides), vp, vp, vp]
     got = lib.swarm_abi_version()
     if got != ABI_VERSION:
         raise NativeLibraryError(f"{p}: ABI version {got}, expected {ABI_VERSION}")

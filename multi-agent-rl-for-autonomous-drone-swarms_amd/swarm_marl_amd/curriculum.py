@@ -9,12 +9,19 @@ enforce.  Here a stage is a VecSwarm of E envs built from that env_config (stage
 M, i.e. the tensor shapes, so each stage is its own batch) with an EvalTracker; the window
 metrics come from the device eval records and `advance()` moves on by iteration count, or by
 the criteria when asked to.
+
+Stages that share N (stages 1-2 of curriculum_v1 are both N = 3) can also run side by side in ONE
+batch: `mixed_stage_batch` gives each env its stage's num_obstacles / max_steps / world_size as
+per-env parameters (swarm_env_cfg_t), so a curriculum can keep a replay fraction of earlier
+stages without a second launch.
 """
 from __future__ import annotations
 
 import math
 from pathlib import Path
 from typing import Any
+
+import numpy as np
 
 from .eval_metrics import EvalTracker, aggregate_records
 from .vec_env import VecSwarm
@@ -44,6 +51,42 @@ def stage_env_config(cfg: dict, index: int, base_seed: int = 0) -> dict[str, Any
     env_cfg = dict(cfg["stages"][index].get("env_config", {}))
     env_cfg["seed"] = int(base_seed + index)
     return env_cfg
+
+
+STAGE_PARAMS = ("world_size", "dt", "max_speed", "max_accel", "obstacle_radius", "max_steps", "num_obstacles")
+
+
+def mixed_stage_batch(cfg: dict, stage_of_env, *, base_seed: int = 0, seed: int | None = None, device=None,
+                      **vec_kw):
+    """One VecSwarm whose env e runs stage stage_of_env[e]'s env_config (stages must share
+    num_drones and the env_config keys other than STAGE_PARAMS).  Returns (vec, overrides): the
+    batch holds max(num_obstacles) obstacle slots and every stage parameter as a per-env value;
+    `overrides` maps each parameter to its [E] numpy array."""
+    stages = np.asarray(stage_of_env, dtype=np.int64)
+    if stages.ndim != 1 or len(stages) == 0:
+        raise ValueError("stage_of_env must be a non-empty 1-D sequence of stage indices")
+    used = sorted(set(int(i) for i in stages))
+    if used[0] < 0 or used[-1] >= len(cfg["stages"]):
+        raise ValueError(f"stage index out of range [0, {len(cfg['stages'])})")
+    env_cfgs = {i: stage_env_config(cfg, i, base_seed) for i in used}
+    n_set = {int(c.get("num_drones", 3)) for c in env_cfgs.values()}
+    if len(n_set) != 1:
+        raise ValueError(f"stages {used} differ in num_drones {sorted(n_set)}: they cannot share a batch")
+    rest = [{k: v for k, v in c.items() if k not in STAGE_PARAMS + ("seed",)} for c in env_cfgs.values()]
+    if any(r != rest[0] for r in rest):
+        raise ValueError("stages differ in fields other than " + ", ".join(STAGE_PARAMS))
+    from .envs.common import DroneEnvConfig
+    batch = dict(rest[0])
+    batch["num_obstacles"] = max(int(c.get("num_obstacles", DroneEnvConfig.num_obstacles)) for c in env_cfgs.values())
+    defaults = DroneEnvConfig()
+    over = {}
+    for k in STAGE_PARAMS:
+        vals = [env_cfgs[int(i)].get(k, getattr(defaults, k)) for i in stages]
+        over[k] = np.asarray(vals, dtype=np.int32 if k in ("max_steps", "num_obstacles") else np.float64)
+    vec = VecSwarm(len(stages), batch, device=device, auto_reset=True,
+                   seed=int(base_seed if seed is None else seed), **vec_kw)
+    vec.set_env_config(**over)
+    return vec, over
 
 
 def criteria_met(metrics: dict, criteria: dict | None) -> bool:

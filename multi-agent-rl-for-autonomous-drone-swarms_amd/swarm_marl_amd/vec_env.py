@@ -160,6 +160,8 @@ class VecSwarm:
         # zero by every launch)
         self.work = (torch.zeros((self.groups, nat.WORK_WORDS), dtype=torch.int32, **kw)
                      if self.persistent else None)
+        # per-env parameter records ([E, 64] bytes of swarm_env_cfg_t; set_env_config)
+        self.env_cfg = self.env_cfg_next = None
         # ---- outputs (persistent buffers)
         outs = [("obs", (e, n, d), f32), ("reward", (e, n), f32)]
         if with_infos:
@@ -214,6 +216,7 @@ class VecSwarm:
             s.active, s.step_count = off(self.active, lo), off(self.step_count, lo)
             s.episode, s.damping = off(self.episode, lo), off(self.damping, lo)
             s.work = None if self.work is None else _ptr(self.work[g])
+            s.env_cfg, s.env_cfg_next = off(self.env_cfg, lo), off(self.env_cfg_next, lo)
             o = nat.SwarmOut()
             o.obs, o.reward = off(self.obs, lo), off(self.reward, lo)
             o.terminated, o.truncated = off(self.terminated, lo), off(self.truncated, lo)
@@ -347,6 +350,83 @@ class VecSwarm:
                 raise ValueError(f"{name}: shape {tuple(src.shape)} != {tuple(dst.shape)}")
             dst.copy_(src.to(dtype=dst.dtype), non_blocking=False)
 
+    # ------------------------------------------------------------------ per-env parameters
+    def set_env_config(self, *, env_mask: torch.Tensor | None = None, next_episode: bool = False,
+                       **values) -> None:
+        """Per-env parameters (curriculum stages and domain randomisation as
+        per-env tensors).  `values` maps any of world_size, dt, max_speed, max_accel,
+        obstacle_radius (float), max_steps, num_obstacles (int, 0..num_obstacles of the batch) to a
+        scalar or an [E] array; unnamed fields take the batch config.  The records of the masked
+        envs (all if None) are derived on the device (swarm_env_cfg_set, no host sync).
+
+        next_episode=False sets the CURRENT parameters (they apply from the next step / reset on;
+        a curriculum mix keeps them across resets).  next_episode=True sets the parameters each
+        env's NEXT episode starts with: every reset (auto or explicit) copies them in — the hook
+        for per-episode randomisation (domain_randomization.py).  The step then runs the generic
+        kernel."""
+        unknown = set(values) - set(nat.ENV_OVERRIDE_FIELDS)
+        if unknown:
+            raise ValueError(f"unknown per-env parameters {sorted(unknown)}; "
+                             f"supported: {nat.ENV_OVERRIDE_FIELDS}")
+        if self.dynamics == "physics" and values.get("dt") is not None:
+            raise ValueError("per-env dt applies to the kinematic integrator only (physics substeps are "
+                             "uniform)")
+        e = self.num_envs
+        self.join()
+        rebind = False
+        if self.env_cfg is None:
+            self.env_cfg = torch.zeros((e, nat.ENV_CFG_BYTES), dtype=torch.uint8, device=self.device)
+            self._env_cfg_write(self.env_cfg, {}, None)  # uniform records first
+            rebind = True
+        if next_episode and self.env_cfg_next is None:
+            self.env_cfg_next = torch.zeros_like(self.env_cfg)
+            self.env_cfg_next.copy_(self.env_cfg)
+            rebind = True
+        if rebind:
+            self._bind()
+        self._env_cfg_write(self.env_cfg_next if next_episode else self.env_cfg, values, env_mask)
+
+    def _env_cfg_write(self, dst: torch.Tensor, values: dict, env_mask) -> None:
+        e = self.num_envs
+        ov = nat.SwarmEnvOverrides()
+        keep = []
+        for name in nat.ENV_OVERRIDE_FIELDS:
+            v = values.get(name)
+            if v is None:
+                continue
+            dt = torch.int32 if name in ("max_steps", "num_obstacles") else torch.float64
+            t = torch.as_tensor(v, dtype=dt).to(self.device)
+            if t.dim() == 0:
+                t = t.expand(e)
+            if tuple(t.shape) != (e,):
+                raise ValueError(f"{name}: expected a scalar or shape ({e},), got {tuple(t.shape)}")
+            t = t.contiguous()
+            keep.append(t)
+            setattr(ov, name, t.data_ptr())
+        mp = self._mask_ptr(env_mask)
+        for g, (lo, hi) in enumerate(self.group_slices):
+            og = nat.SwarmEnvOverrides()
+            for name in nat.ENV_OVERRIDE_FIELDS:
+                ptr = getattr(ov, name)
+                setattr(og, name, None if ptr is None else ptr + lo * (4 if name in ("max_steps", "num_obstacles")
+                                                                        else 8))
+            rc = self.lib.swarm_env_cfg_set(ctypes.byref(self._gparams[g]), ctypes.byref(og),
+                                            None if mp is None else mp + lo,
+                                            dst.data_ptr() + lo * nat.ENV_CFG_BYTES, self._stream())
+            nat.check(rc, self.lib)
+        self._keep_cfg = keep  # the launches read them asynchronously
+
+    def env_config(self, next_episode: bool = False) -> dict[str, torch.Tensor] | None:
+        """Per-env parameters as [E] tensors (views of the records), or None if unset."""
+        rec = self.env_cfg_next if next_episode else self.env_cfg
+        if rec is None:
+            return None
+        f = rec.view(torch.float32)
+        i = rec.view(torch.int32)
+        d = rec.view(torch.float64)
+        return dict(world_size=d[:, 7], dt=f[:, 3], max_speed=d[:, 6], max_accel=f[:, 5],
+                    max_steps=i[:, 9], num_obstacles=i[:, 10], half_w=f[:, 0], s_obst=f[:, 7])
+
     def state_dict(self) -> dict[str, torch.Tensor]:
         return dict(pos=self.pos, vel=self.vel, goal=self.goal, obstacles=self.obstacles,
                     active=self.active, step_count=self.step_count, episode=self.episode,
@@ -366,6 +446,8 @@ class VecSwarm:
         With env groups: the kernel of group 0."""
         li = self.group_launch_info[0]
         kid = int(li.kernel_id)
+        if self.env_cfg is not None:  # per-env parameters: always the generic kernel
+            kid = nat.KERNEL_GENERIC
         if kid == nat.KERNEL_STEP64_PERSISTENT and self.persistent:
             return "swarm_step64<32>"
         if kid in (nat.KERNEL_STEP64, nat.KERNEL_STEP64_PERSISTENT):

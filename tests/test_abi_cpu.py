@@ -60,7 +60,7 @@ def _params(nat, lib, **kw):
 
 def test_abi_version_and_defaults(nat, lib):
     from swarm_marl_amd.envs.common import DroneEnvConfig
-    assert lib.swarm_abi_version() == nat.ABI_VERSION == 3
+    assert lib.swarm_abi_version() == nat.ABI_VERSION == 4
     p = _params(nat, lib)
     c = DroneEnvConfig()
     for name in ("max_steps", "num_obstacles", "sensed_obstacles", "neighbor_k"):
@@ -136,3 +136,43 @@ def test_null_arguments_and_empty_batch(nat, lib):
 def test_missing_library_fails_loudly(nat, tmp_path):
     with pytest.raises(nat.NativeLibraryError):
         nat.load_library(tmp_path / "libswarm_mi355x.so")
+
+
+def test_env_cfg_layout_matches_header(nat, tmp_path):
+    """ctypes mirrors of the per-env records agree with the C compiler's layout of the header."""
+    fields = [f for f, _ in nat.SwarmEnvCfg._fields_]
+    src = tmp_path / "layout.c"
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "swarm_mi355x.h"', "int main(void) {",
+             'printf("%zu %zu %zu\\n", sizeof(swarm_env_cfg_t), sizeof(swarm_state_t), sizeof(swarm_env_overrides_t));']
+    lines += [f'printf("%zu\\n", offsetof(swarm_env_cfg_t, {f}));' for f in fields]
+    lines += [f'printf("%zu\\n", offsetof(swarm_state_t, {f}));' for f, _ in nat.SwarmState._fields_]
+    lines += ["return 0; }"]
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    sizes, rest = [int(x) for x in out[:3]], [int(x) for x in out[3:]]
+    assert sizes == [ctypes.sizeof(nat.SwarmEnvCfg), ctypes.sizeof(nat.SwarmState),
+                     ctypes.sizeof(nat.SwarmEnvOverrides)]
+    assert sizes[0] == nat.ENV_CFG_BYTES == 64
+    assert rest[:len(fields)] == [getattr(nat.SwarmEnvCfg, f).offset for f in fields]
+    assert rest[len(fields):] == [getattr(nat.SwarmState, f).offset for f, _ in nat.SwarmState._fields_]
+
+
+def test_env_cfg_set_validation(nat, lib):
+    ov = nat.SwarmEnvOverrides()
+    p0 = _params(nat, lib, num_envs=0)
+    assert lib.swarm_env_cfg_set(ctypes.byref(p0), ctypes.byref(ov), None, None, None) == 0  # empty: no-op
+    p = _params(nat, lib, num_envs=4)
+    assert lib.swarm_env_cfg_set(ctypes.byref(p), None, None, None, None) == nat.SWARM_ENULL
+    assert lib.swarm_env_cfg_set(ctypes.byref(p), ctypes.byref(ov), None, None, None) == nat.SWARM_ENULL
+    assert lib.swarm_env_cfg_set(ctypes.byref(_params(nat, lib, num_envs=4, num_drones=0)), ctypes.byref(ov),
+                                 None, None, None) == nat.SWARM_ELIMIT
+    # a next-episode record without a current one is rejected before any launch
+    s, o = nat.SwarmState(), nat.SwarmOut()
+    for name in ("pos", "vel", "goal", "obstacles", "active", "step_count", "episode"):
+        setattr(s, name, 16)
+    o.obs, o.reward, o.terminated, o.truncated, o.env_done = 16, 16, 16, 16, 16
+    s.env_cfg_next = 64
+    assert lib.swarm_step(ctypes.byref(p), ctypes.byref(s), 16, None, ctypes.byref(o), None) == nat.SWARM_ENULL
+    assert b"env_cfg" in lib.swarm_last_error()
