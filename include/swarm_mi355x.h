@@ -295,9 +295,12 @@ const char* swarm_policy_last_error(void);
  */
 #define SWARM_EVAL_LIVE 1u       /* status: an episode is being accumulated */
 #define SWARM_EVAL_COLLIDED 2u   /* status: an observed agent reported a collision */
-#define SWARM_EVAL_RECORD 8      /* doubles per record: global env index, success, collision_free, time_to_goal
+#define SWARM_EVAL_RECORD 9      /* doubles per record: global env index, success, collision_free, time_to_goal
                                     (NaN if never all-reached), formation_error, path_efficiency,
-                                    episode_reward, steps */
+                                    episode_reward, steps, update_index of the closing update */
+#define SWARM_EVAL_SEGMENTS 64   /* record counters: an episode of global env g is appended to segment
+                                    g % 64 (64 counters on distinct lines instead of one contended
+                                    device-scope atomic) */
 
 typedef struct swarm_eval {
   double* ep_reward;      /* [E] sum over steps of the mean reward of the stepped agents */
@@ -309,10 +312,12 @@ typedef struct swarm_eval {
   float* goal;            /* [E,N,3] start + obs[6:9] (the reference's goal estimate) */
   float* last;            /* [E,N,3] last observed positions */
   double* traveled;       /* [E,N]   path length */
-  double* records;        /* [capacity, SWARM_EVAL_RECORD] finished episodes */
-  uint32_t* count;        /* [1] records appended (may exceed capacity: the rest are dropped) */
-  int32_t capacity;
-  int32_t reserved;
+  double* records;        /* [capacity, SWARM_EVAL_RECORD] finished episodes; segment s owns rows
+                             [s*C, (s+1)*C), C = capacity / SWARM_EVAL_SEGMENTS */
+  uint32_t* count;        /* [SWARM_EVAL_SEGMENTS] records appended per segment (may exceed C: the
+                             rest are dropped) */
+  int32_t capacity;       /* a multiple of SWARM_EVAL_SEGMENTS */
+  int32_t update_index;   /* stamped into the records this update closes (the caller counts updates) */
 } swarm_eval_t;
 
 /* Start an episode in the masked envs (all if NULL) from the current obs (after a reset). */

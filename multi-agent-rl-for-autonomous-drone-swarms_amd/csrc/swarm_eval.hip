@@ -12,7 +12,8 @@
 //     dict holds no observations: the all-reached test then passes vacuously — the
 //     reference's behaviour, kept),
 //   * at the episode's end one record {env, success, collision-free, time-to-goal, formation
-//     error, path efficiency, reward, steps} is appended (vector atomic on the record counter);
+//     error, path efficiency, reward, steps, update} is appended to one of 64 record segments
+//     (vector atomic on that segment's counter);
 //     an env auto-reset in the same launch starts its next episode from the new observations.
 // Distances follow the reference's float(np.linalg.norm(a - b)) of float32 vectors (sdot: f32
 // products, f64 sum, f32 sqrt); sums are f64.
@@ -30,11 +31,28 @@
 namespace {
 
 constexpr int EVAL_THREADS = 64;
+#ifndef SWARM_EVAL_ABLATE  // diagnostics (tools/): 1 = skip the formation error, 2 = skip episode
+#define SWARM_EVAL_ABLATE 0  // ends, 3 = no counter atomic (slot 0 of the segment), 4 = 1 + 2, 5 = return
+#endif                       // after the first loads
 constexpr int EVAL_MAX_N = 1024;
 
 __device__ __forceinline__ float norm1d(float x, float y, float z) {
   const float xx = x * x, yy = y * y, zz = z * z;
   return __builtin_sqrtf((float)(((double)xx + (double)yy) + (double)zz));  // IEEE sqrt
+}
+
+// The same float as norm1d, with the correctly rounded square root as swarm_kernel.hip's
+// sqrt_rn (v_sqrt_f32 within 1 ulp + one correction step; OCML's scaling path below 2^-96).
+__device__ __forceinline__ float norm1d_fast(float x, float y, float z) {
+  const float xx = x * x, yy = y * y, zz = z * z;
+  const float s = (float)(((double)xx + (double)yy) + (double)zz);
+  if (__builtin_expect(__ballot(!(s >= 0x1p-96f || s == 0.0f)) != 0, 0)) return __builtin_sqrtf(s);
+  float r = __builtin_amdgcn_sqrtf(s);
+  const float rm = __uint_as_float(__float_as_uint(r) - 1u), rp = __uint_as_float(__float_as_uint(r) + 1u);
+  const float em = __builtin_fmaf(-rm, r, s), ep = __builtin_fmaf(-rp, r, s);
+  r = (em <= 0.0f) ? rm : r;
+  r = (ep > 0.0f) ? rp : r;
+  return r;
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -87,36 +105,74 @@ __global__ void __launch_bounds__(EVAL_THREADS) eval_begin_kernel(const EvalArgs
   begin_env(a, e, threadIdx.x);
 }
 
+// One wave per env.  Every global load of the step is issued in one batch at the top (the env's
+// accumulators, the agents' flags / reward / observed position / last position / path length,
+// and — known from env_done before anything else — the start / goal rows of an ending episode and
+// the goal columns of a restarting one): the kernel is latency-bound (all 8192 waves of the
+// headline batch are resident at once), so the chain of dependent memory round trips, not the
+// bytes, sets its time.  A restart writes the new episode's start rows in the same pass.
 __global__ void __launch_bounds__(EVAL_THREADS) eval_update_kernel(const EvalArgs a) {
-  __shared__ float4 pos[EVAL_MAX_N];  // agents with an observation this step (x, y, z, has)
+  // agents with an observation this step (x, y, z, has); N float4 of dynamic LDS, so that the
+  // LDS of a small swarm does not cap the waves per CU (a static EVAL_MAX_N array did: 16 KB)
+  extern __shared__ float4 pos[];
   const int e = blockIdx.x;
   const int t = threadIdx.x;
   const swarm_eval_t& v = a.ev;
   const uint8_t status = v.status[e];  // uniform
-  if (!(status & SWARM_EVAL_LIVE)) return;
   const uint8_t done = a.env_done[e];
-  // ---- per-agent votes and the observed positions
-  double rsum = 0.0;
+  const double ep_reward0 = v.ep_reward[e];
+  const double fe_sum0 = v.fe_sum[e];
+  const int steps0 = v.ep_steps[e];
+  const int reached0 = v.reached_step[e];
+  if (!(status & SWARM_EVAL_LIVE) || SWARM_EVAL_ABLATE == 5) return;
+  const bool ends = (done & (SWARM_ENV_TERMINATED | SWARM_ENV_TRUNCATED)) != 0 && SWARM_EVAL_ABLATE != 2 &&
+                    SWARM_EVAL_ABLATE != 4;
+  const bool restarts = ends && (done & SWARM_ENV_RESET) != 0;
+  // ---- per-agent votes, path length, observed positions; path efficiency and the next
+  // episode's start rows when the episode ends here
+  double rsum = 0.0, pe = 0.0;
   int n_st = 0, n_obs = 0, coll = 0, not_reached = 0;
   for (int i = t; i < a.N; i += EVAL_THREADS) {
     const size_t r = (size_t)e * a.N + i;
+    const float* o = a.obs + r * a.D;
     const uint8_t fl = a.info_flags[r];
+    const float rw = a.reward[r];
+    const float ox = o[0], oy = o[1], oz = o[2];
+    const float lx = v.last[3 * r], ly = v.last[3 * r + 1], lz = v.last[3 * r + 2];
+    double tr = v.traveled[r];
+    float sx = 0.f, sy = 0.f, sz = 0.f, gx = 0.f, gy = 0.f, gz = 0.f, rx = 0.f, ry = 0.f, rz = 0.f;
+    if (ends) {
+      sx = v.start[3 * r]; sy = v.start[3 * r + 1]; sz = v.start[3 * r + 2];
+      gx = v.goal[3 * r]; gy = v.goal[3 * r + 1]; gz = v.goal[3 * r + 2];
+    }
+    if (restarts) { rx = o[6]; ry = o[7]; rz = o[8]; }
     if (fl & SWARM_AGENT_STEPPED) {
-      rsum += (double)a.reward[r];
+      rsum += (double)rw;
       ++n_st;
     }
     const bool has = (fl & SWARM_AGENT_HAS_OBS) != 0;
     float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
     if (has) {
-      const float* o = a.obs + r * a.D;
-      p = make_float4(o[0], o[1], o[2], 1.f);
+      p = make_float4(ox, oy, oz, 1.f);
       ++n_obs;
       coll |= (fl & SWARM_AGENT_COLLISION) ? 1 : 0;
       not_reached |= (fl & SWARM_AGENT_REACHED) ? 0 : 1;
-      v.traveled[r] += (double)norm1d(v.last[3 * r] - p.x, v.last[3 * r + 1] - p.y, v.last[3 * r + 2] - p.z);
-      v.last[3 * r] = p.x; v.last[3 * r + 1] = p.y; v.last[3 * r + 2] = p.z;
+      tr += (double)norm1d(lx - ox, ly - oy, lz - oz);
     }
     pos[i] = p;
+    if (ends) {
+      const float straight = norm1d(sx - gx, sy - gy, sz - gz);
+      pe += tr > 1e-8 ? (double)straight / tr : 0.0;
+    }
+    if (restarts) {  // the obs rows are the new episode's first observation (every agent)
+      v.start[3 * r] = ox; v.start[3 * r + 1] = oy; v.start[3 * r + 2] = oz;
+      v.goal[3 * r] = ox + rx; v.goal[3 * r + 1] = oy + ry; v.goal[3 * r + 2] = oz + rz;
+      v.last[3 * r] = ox; v.last[3 * r + 1] = oy; v.last[3 * r + 2] = oz;
+      v.traveled[r] = 0.0;
+    } else if (has) {
+      v.traveled[r] = tr;
+      v.last[3 * r] = ox; v.last[3 * r + 1] = oy; v.last[3 * r + 2] = oz;
+    }
   }
   __syncthreads();
   rsum = wave_sum(rsum);
@@ -126,7 +182,27 @@ __global__ void __launch_bounds__(EVAL_THREADS) eval_update_kernel(const EvalArg
   not_reached = __any(not_reached) ? 1 : 0;
   // ---- formation error of the observed set (evaluate_protocol.py:103-116)
   double fe = 0.0;
-  if (n_obs > 1) {
+  if (SWARM_EVAL_ABLATE == 1 || SWARM_EVAL_ABLATE == 4) {
+  } else if (n_obs > 1 && a.N == EVAL_THREADS) {
+    // one drone per lane: symmetric rotations.  At rotation r lane t measures the pair
+    // (t, t+r) once and hands the distance to lane t+r (ds_bpermute); r = 32 pairs each lane
+    // with its own opposite, measured by both.  Distances are symmetric bit for bit
+    // (|a-b| = |b-a| per component), so each drone sums exactly the reference's terms; only the
+    // f64 summation order differs (np.mean's pairwise order is not reproduced: 1e-9 relative).
+    const float4 p = pos[t];
+    double s_own = 0.0, s_mir = 0.0;  // two chains of dependent f64 adds instead of one
+#pragma unroll 8
+    for (int r = 1; r <= 32; ++r) {
+      const float4 q = pos[(t + r) & (EVAL_THREADS - 1)];
+      float d = norm1d_fast(p.x - q.x, p.y - q.y, p.z - q.z);
+      d = (p.w != 0.f && q.w != 0.f) ? d : -1.f;  // -1: pair not in the observed set
+      const float dm = __shfl(d, (t - r) & (EVAL_THREADS - 1));  // pair (t-r, t), from lane t-r
+      if (d >= 0.f) s_own += fabs((double)d - a.spacing);
+      if (r < 32 && dm >= 0.f) s_mir += fabs((double)dm - a.spacing);
+    }
+    const double acc = p.w != 0.f ? (s_own + s_mir) / (double)(n_obs - 1) : 0.0;
+    fe = wave_sum(acc) / (double)n_obs;
+  } else if (n_obs > 1) {
     double acc = 0.0;
     for (int i = t; i < a.N; i += EVAL_THREADS) {
       const float4 p = pos[i];
@@ -141,51 +217,44 @@ __global__ void __launch_bounds__(EVAL_THREADS) eval_update_kernel(const EvalArg
     }
     fe = wave_sum(acc) / (double)n_obs;
   }
-  int steps = 0, reached = -1;
-  double ep_reward = 0.0, fe_sum = 0.0;
-  if (t == 0) {
-    ep_reward = v.ep_reward[e] + (n_st > 0 ? rsum / (double)n_st : 0.0);
-    fe_sum = v.fe_sum[e] + fe;
-    steps = v.ep_steps[e] + 1;
-    reached = v.reached_step[e];
-    if (!not_reached && reached < 0) reached = steps;
+  if (ends) pe = wave_sum(pe) / (double)a.N;
+  if (t != 0) return;
+  const double ep_reward = ep_reward0 + (n_st > 0 ? rsum / (double)n_st : 0.0);
+  const double fe_sum = fe_sum0 + fe;
+  const int steps = steps0 + 1;
+  int reached = reached0;
+  if (!not_reached && reached < 0) reached = steps;
+  if (!ends) {
     v.ep_reward[e] = ep_reward;
     v.fe_sum[e] = fe_sum;
     v.ep_steps[e] = steps;
     v.reached_step[e] = reached;
     if (coll) v.status[e] = status | SWARM_EVAL_COLLIDED;
+    return;
   }
-  if (!(done & (SWARM_ENV_TERMINATED | SWARM_ENV_TRUNCATED))) return;
-  // ---- episode end: path efficiency over every agent, one record
-  double pe = 0.0;
-  for (int i = t; i < a.N; i += EVAL_THREADS) {
-    const size_t r = (size_t)e * a.N + i;
-    const float straight = norm1d(v.start[3 * r] - v.goal[3 * r], v.start[3 * r + 1] - v.goal[3 * r + 1],
-                                  v.start[3 * r + 2] - v.goal[3 * r + 2]);
-    const double tr = v.traveled[r];
-    pe += tr > 1e-8 ? (double)straight / tr : 0.0;
+  // ---- episode end: one record; a restarting env opens its next episode
+  const bool collided = coll || (status & SWARM_EVAL_COLLIDED);
+  const long long genv = a.env_offset + e;
+  const unsigned seg = (unsigned)(genv % SWARM_EVAL_SEGMENTS);
+  const unsigned seg_cap = (unsigned)v.capacity / SWARM_EVAL_SEGMENTS;
+  const unsigned k = SWARM_EVAL_ABLATE == 3 ? 0u : atomicAdd(v.count + seg, 1u);
+  if (k < seg_cap) {
+    double* rec = v.records + ((size_t)seg * seg_cap + k) * SWARM_EVAL_RECORD;
+    rec[0] = (double)genv;  // global env index
+    rec[1] = (!collided && reached >= 0) ? 1.0 : 0.0;
+    rec[2] = collided ? 0.0 : 1.0;
+    rec[3] = reached >= 0 ? (double)reached : __builtin_nan("");
+    rec[4] = fe_sum / (double)steps;
+    rec[5] = pe;
+    rec[6] = ep_reward;
+    rec[7] = (double)steps;
+    rec[8] = (double)v.update_index;
   }
-  pe = wave_sum(pe) / (double)a.N;
-  if (t == 0) {
-    const bool collided = coll || (status & SWARM_EVAL_COLLIDED);
-    const unsigned k = atomicAdd(v.count, 1u);
-    if (k < (unsigned)v.capacity) {
-      double* rec = v.records + (size_t)k * SWARM_EVAL_RECORD;
-      rec[0] = (double)(a.env_offset + e);  // global env index
-      rec[1] = (!collided && reached >= 0) ? 1.0 : 0.0;
-      rec[2] = collided ? 0.0 : 1.0;
-      rec[3] = reached >= 0 ? (double)reached : __builtin_nan("");
-      rec[4] = fe_sum / (double)steps;
-      rec[5] = pe;
-      rec[6] = ep_reward;
-      rec[7] = (double)steps;
-    }
-    v.status[e] = 0;
-  }
-  if (done & SWARM_ENV_RESET) {  // auto-reset in the same launch: the next episode starts now
-    __syncthreads();
-    begin_env(a, e, t);
-  }
+  v.ep_reward[e] = 0.0;
+  v.fe_sum[e] = 0.0;
+  v.ep_steps[e] = 0;
+  v.reached_step[e] = -1;
+  v.status[e] = restarts ? SWARM_EVAL_LIVE : 0;
 }
 
 thread_local char g_eerr[256] = "";
@@ -206,7 +275,8 @@ int make_args(const swarm_params_t* p, const swarm_eval_t* ev, const swarm_out_t
   if (!ev->ep_reward || !ev->ep_steps || !ev->reached_step || !ev->status || !ev->fe_sum || !ev->start || !ev->goal ||
       !ev->last || !ev->traveled || !ev->records || !ev->count)
     return efail(SWARM_ENULL, "an eval state buffer is NULL");
-  if (ev->capacity < 0) return efail(SWARM_EINVAL, "capacity < 0");
+  if (ev->capacity < 0 || ev->capacity % SWARM_EVAL_SEGMENTS != 0)
+    return efail(SWARM_EINVAL, "capacity must be a non-negative multiple of %d", SWARM_EVAL_SEGMENTS);
   a->E = p->num_envs;
   a->N = p->num_drones;
   a->D = 9 + 4 * (p->neighbor_k > 0 ? p->neighbor_k : 0) + 4 * (p->sensed_obstacles > 0 ? p->sensed_obstacles : 0);
@@ -244,7 +314,8 @@ int swarm_eval_update(const swarm_params_t* p, const swarm_eval_t* ev, const swa
   if (!o->reward || !o->info_flags || !o->env_done)
     return efail(SWARM_ENULL, "out.reward/info_flags/env_done required (build the env with infos)");
   if (a.E == 0) return SWARM_OK;
-  hipLaunchKernelGGL(eval_update_kernel, dim3(a.E), dim3(EVAL_THREADS), 0, (hipStream_t)hip_stream, a);
+  hipLaunchKernelGGL(eval_update_kernel, dim3(a.E), dim3(EVAL_THREADS), (unsigned)(a.N * sizeof(float4)),
+                     (hipStream_t)hip_stream, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? SWARM_OK : efail(SWARM_EHIP, "eval_update launch: %s", hipGetErrorString(e));
 }

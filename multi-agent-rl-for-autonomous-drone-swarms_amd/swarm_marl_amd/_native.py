@@ -52,7 +52,8 @@ POLICY_ACT_MEAN = 0
 POLICY_ACT_SAMPLE = 1
 EVAL_LIVE = 1
 EVAL_COLLIDED = 2
-EVAL_RECORD = 8
+EVAL_RECORD = 9
+EVAL_SEGMENTS = 64
 
 # every symbol include/swarm_mi355x.h declares
 EXPORTED_SYMBOLS = (
@@ -143,7 +144,7 @@ class SwarmPolicy(ctypes.Structure):
 class SwarmEval(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name in
                 ("ep_reward", "ep_steps", "reached_step", "status", "fe_sum", "start", "goal", "last",
-                 "traveled", "records", "count")] + [("capacity", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                 "traveled", "records", "count")] + [("capacity", ctypes.c_int32), ("update_index", ctypes.c_int32)]
 
 
 class SwarmLaunchInfo(ctypes.Structure):

@@ -30,11 +30,11 @@ from . import _native as nat
 from .vec_env import VecSwarm
 
 FIELDS = ("env", "success", "collision_free", "time_to_goal", "formation_error", "path_efficiency",
-          "episode_reward", "steps")
+          "episode_reward", "steps", "update")
 
 
 def aggregate_records(rec: np.ndarray) -> dict:
-    """evaluate_protocol.py:334-350 `_aggregate` over records [n, 8] (FIELDS order)."""
+    """evaluate_protocol.py:334-350 `_aggregate` over records [n, >= 8] (FIELDS order)."""
     if len(rec) == 0:
         return {"episodes": 0, "success_rate": 0.0, "collision_free_rate": 0.0, "mean_time_to_goal": math.nan,
                 "formation_error": 0.0, "path_efficiency": 0.0, "episode_reward_mean": 0.0,
@@ -70,9 +70,13 @@ class EvalTracker:
         self.goal = torch.zeros_like(self.start)
         self.last = torch.zeros_like(self.start)
         self.traveled = torch.zeros((e, n), **f64)
-        self.capacity = int(capacity)
-        self.records_buf = torch.zeros((max(self.capacity, 1), nat.EVAL_RECORD), **f64)
-        self.count = torch.zeros(1, dtype=torch.int32, device=dev)
+        seg = nat.EVAL_SEGMENTS
+        # segment s holds the episodes of global envs g with g % 64 == s: capacity per segment
+        # sized for the busiest one (ceil(E / 64) envs, `capacity` episodes per env on average)
+        self.capacity = max(seg, -(-int(capacity) // seg) * seg)
+        self.records_buf = torch.zeros((self.capacity, nat.EVAL_RECORD), **f64)
+        self.count = torch.zeros(seg, dtype=torch.int32, device=dev)
+        self.updates = 0
         c = nat.SwarmEval()
         for name in ("ep_reward", "ep_steps", "reached_step", "status", "fe_sum", "start", "goal", "last",
                      "traveled", "count"):
@@ -96,12 +100,14 @@ class EvalTracker:
     def update(self) -> None:
         """Accumulate the last step (call after every VecSwarm.step)."""
         self.vec.join()
+        self.updates += 1
         for g in range(self.vec.groups):
             nat.check(self.lib.swarm_eval_update(ctypes.byref(self.vec._gparams[g]), ctypes.byref(self._group_c(g)),
                                                  ctypes.byref(self.vec._gout[g]), self._stream()), self.lib,
                       which="eval")
 
     def _group_c(self, g: int) -> nat.SwarmEval:
+        self._c.update_index = self.updates
         if self.vec.groups == 1:
             return self._c
         lo = self.vec.group_slices[g][0]
@@ -111,14 +117,20 @@ class EvalTracker:
             t = getattr(self, name)
             setattr(c, name, t.data_ptr() + lo * t.stride(0) * t.element_size())
         c.records, c.count, c.capacity = self.records_buf.data_ptr(), self.count.data_ptr(), self.capacity
+        c.update_index = self.updates
         return c
 
     def records(self) -> np.ndarray:
-        """Finished-episode records [n, 8] (FIELDS), in completion order."""
-        n = int(self.count.item())
-        if n > self.capacity:
-            raise RuntimeError(f"{n} episodes finished but the record buffer holds {self.capacity}")
-        return self.records_buf[:n].cpu().numpy()
+        """Finished-episode records [n, 9] (FIELDS), in completion order: by the update that
+        closed them, then by global env index (deterministic)."""
+        counts = self.count.cpu().numpy().astype(np.int64)
+        seg_cap = self.capacity // nat.EVAL_SEGMENTS
+        if counts.max(initial=0) > seg_cap:
+            raise RuntimeError(f"{int(counts.max())} episodes finished in one record segment, which holds "
+                               f"{seg_cap} (EvalTracker capacity {self.capacity}); raise the capacity")
+        buf = self.records_buf.cpu().numpy()
+        rec = np.concatenate([buf[s * seg_cap:s * seg_cap + int(c)] for s, c in enumerate(counts)], axis=0)
+        return rec[np.lexsort((rec[:, 0], rec[:, 8]))]
 
     def aggregate(self) -> dict:
         return aggregate_records(self.records())

@@ -18,7 +18,7 @@ K = int(sys.argv[3]) if len(sys.argv) > 3 else 200
 dev = torch.device("cuda", 0)
 vec = VecSwarm(E, {"num_drones": N}, device=dev, auto_reset=True, seed=0, with_infos=True)
 vec.reset()
-ev = EvalTracker(vec, capacity=1 << 20)
+ev = EvalTracker(vec, capacity=1 << 21)
 ev.begin()
 g = torch.Generator(device=dev).manual_seed(1)
 ring = [torch.rand((E, N, 3), device=dev, generator=g) * 2 - 1 for _ in range(8)]
@@ -39,5 +39,5 @@ for mode in ("step", "step+eval", "step", "step+eval"):
     torch.cuda.synchronize()
     res[mode] = a.elapsed_time(b) / K
 print(json.dumps({"E": E, "N": N, "ms_per_step": res["step"], "ms_per_step_with_eval": res["step+eval"],
-                  "eval_ms_per_step": res["step+eval"] - res["step"], "episodes_recorded": int(ev.count.item()),
+                  "eval_ms_per_step": res["step+eval"] - res["step"], "episodes_recorded": int(ev.count.sum()),
                   "aggregate": ev.aggregate()}))
