@@ -761,15 +761,23 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       cz = cz + P.g;
       float fac = 1.f;
       if (P.damping_law == 1) fac = (float)pow((double)(1.f - damp), (double)h);
+      // One correctly rounded norm per substep in the common case: the clamp test runs in
+      // squared space (s_vmax: sqrt_rn(s) > vmax exactly when s > s_vmax), and an unclamped
+      // velocity's norm after the clamp is the norm before it, so the damping law reuses it.
+      const bool law0 = P.damping_law == 0;
       for (int s = 0; s < P.substeps; ++s) {
-        const float sp = sqrt_rn(sqsum_1d(vx, vy, vz));
-        if (has && sp > C.max_speed) {
+        const float s_sp = sqsum_1d(vx, vy, vz);
+        float sp2 = 0.f;
+        if (has && s_sp > C.s_vmax) {
+          const float sp = sqrt_rn(s_sp);
           vx = (vx / sp) * C.max_speed;
           vy = (vy / sp) * C.max_speed;
           vz = (vz / sp) * C.max_speed;
+          if (law0) sp2 = sqrt_rn(sqsum_1d(vx, vy, vz));
+        } else if (law0) {
+          sp2 = sqrt_rn(s_sp);
         }
-        if (P.damping_law == 0) {
-          const float sp2 = sqrt_rn(sqsum_1d(vx, vy, vz));
+        if (law0) {
           const float c = damp * (1.f + sp2);
           vx = vx + h * (cx - c * vx);
           vy = vy + h * (cy - c * vy);
