@@ -59,7 +59,7 @@ extern "C" {
 /* kernel actually launched (swarm_launch_info_t.kernel_id) */
 #define SWARM_KERNEL_GENERIC 0  /* swarm_kernel<KIND, DYN, KS, MSL, LM> */
 #define SWARM_KERNEL_STEP64 1   /* swarm_step64_once: N = 64, K = 3, Ms = 4, 4 <= M <= 16, kinematic step;
-                                   one wave per env, 4 envs per workgroup */
+                                   one wave per env, 4 envs per workgroup (physics: swarm_step64_phys_once) */
 #define SWARM_KERNEL_STEP64_PERSISTENT 2  /* swarm_step64: the same step on a persistent grid of
                                    waves_per_simd waves per SIMD with per-XCD env queues
                                    (E > grid; needs state.work, else STEP64 is launched) */

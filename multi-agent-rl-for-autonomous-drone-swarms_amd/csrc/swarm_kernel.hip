@@ -1470,6 +1470,7 @@ struct S64In {
   float px, py, pz, vx, vy, vz, ax, ay, az;  // lane t = drone t
   float ox, oy, oz;                          // lanes t < M: obstacle t
   uint32_t act, has;                         // raw bytes of active / action_mask
+  float damp;                                // physics: drone t's linear damping
   uint32_t gse;  // lanes 0-2: goal x, y, z bits; lane 3: step count; lane 4: episode counter
 };
 
@@ -1492,6 +1493,7 @@ __device__ __forceinline__ S64ArgPtr s64_args() {
   return reinterpret_cast<S64ArgPtr>(v);
 }
 
+template <int DYN = DYN_KIN>
 __device__ __forceinline__ void s64_load(S64ArgPtr A, int env, int t, S64In& c) {
   const float* __restrict__ actions = A->actions;
   const uint8_t* __restrict__ amask = A->amask;
@@ -1512,6 +1514,8 @@ __device__ __forceinline__ void s64_load(S64ArgPtr A, int env, int t, S64In& c) 
   // unconditional loads (no phi with a default value: that would need the data at once)
   c.act = (A->S.active + ea)[t];
   c.has = (amask != nullptr ? amask : A->S.active)[ea + t];  // without a mask: ignored by the body
+  c.damp = 0.f;
+  if constexpr (DYN == DYN_PHYS) c.damp = (A->S.damping + ea)[t];
   const int m = t < A->P.M ? t : A->P.M - 1;  // lanes >= M re-load the last obstacle (unused)
   const float* __restrict__ o = A->S.obstacles + ((size_t)env * A->P.M + m) * 3;
   c.ox = o[0]; c.oy = o[1]; c.oz = o[2];
@@ -1523,7 +1527,7 @@ __device__ __forceinline__ void s64_load(S64ArgPtr A, int env, int t, S64In& c) 
 // LANDED: wait for them (and the queue ticket) after the pair pass, before this env issues any
 // store — vmcnt counts loads and stores in order, so a wait left to the next env's first use would
 // also wait for this env's stores.
-template <int CH, bool LANDED, class Prefetch>
+template <int CH, bool LANDED, class Prefetch, int DYN = DYN_KIN>
 __device__ __forceinline__ void s64_env(const int env, const int M, const S64In& c, float4* __restrict__ ring,
                                         float4* __restrict__ obst, float* __restrict__ stage, const int lane,
                                         Prefetch&& prefetch) {
@@ -1559,9 +1563,48 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   const int n_active = __popcll(__ballot(act));
   STAMP_AT(env, 1);
 
-  // ---- integrate: drone_swarm_env.py:98-117 (identical to swarm_kernel, DYN_KIN)
+  // ---- integrate: drone_swarm_env.py:98-117 (identical to swarm_kernel, DYN_KIN) or the
+  // point-mass physics substeps (identical to swarm_kernel, DYN_PHYS)
   float prev_d = 0.f;
-  if (act) {
+  float damp = c.damp;
+  if constexpr (DYN == DYN_PHYS) {
+    const float h = A->P.h;
+    const float amax = A->P.amax, vmax = A->P.vmax, s_vmax = A->P.s_vmax;
+    const float cx = has ? ax * amax : 0.f;
+    const float cy = has ? ay * amax : 0.f;
+    float cz = has ? az * amax + A->P.gcomp : 0.f;
+    cz = cz + A->P.g;
+    const bool law0 = A->P.damping_law == 0;
+    float fac = 1.f;
+    if (!law0) fac = (float)pow((double)(1.f - damp), (double)h);
+    const int substeps = A->P.substeps;
+    for (int s = 0; s < substeps; ++s) {
+      const float s_sp = sqsum_1d(vx, vy, vz);
+      float sp2 = 0.f;
+      if (has && s_sp > s_vmax) {
+        const float sp = sqrt_rn(s_sp);
+        vx = (vx / sp) * vmax;
+        vy = (vy / sp) * vmax;
+        vz = (vz / sp) * vmax;
+        if (law0) sp2 = sqrt_rn(sqsum_1d(vx, vy, vz));
+      } else if (law0) {
+        sp2 = sqrt_rn(s_sp);
+      }
+      if (law0) {
+        const float cc = damp * (1.f + sp2);
+        vx = vx + h * (cx - cc * vx);
+        vy = vy + h * (cy - cc * vy);
+        vz = vz + h * (cz - cc * vz);
+      } else {
+        vx = (vx + h * cx) * fac;
+        vy = (vy + h * cy) * fac;
+        vz = (vz + h * cz) * fac;
+      }
+      px = px + h * vx;
+      py = py + h * vy;
+      pz = pz + h * vz;
+    }
+  } else if (act) {
     prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
     if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
     ax = clampf(ax, -1.f, 1.f) * A->P.amax;
@@ -1583,12 +1626,13 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     py = py + vy * A->P.dt;
     pz = pz + vz * A->P.dt;
   }
-  if (n_active > 0) {
+  if (DYN == DYN_KIN && n_active > 0) {
     px = clampf(px, A->P.neg_half_w, A->P.half_w);
     py = clampf(py, A->P.neg_half_w, A->P.half_w);
     pz = clampf(pz, A->P.neg_half_w, A->P.half_w);
   }
-  s64_put(ring, soa, t, px, py, pz, act ? 1.f : 0.f);
+  // eligibility: active drones (kinematic), every drone (physics contacts)
+  s64_put(ring, soa, t, px, py, pz, (DYN == DYN_PHYS || act) ? 1.f : 0.f);
   wave_sync();
   prefetch();  // `c` is dead from here on
   if constexpr (SWARM_PRIO_MODE >= 2) __builtin_amdgcn_s_setprio(1);
@@ -1604,7 +1648,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   bool ocoll = false;
   float smin = __builtin_inff();
   double fsum = 0.0;
-  const bool fast = __all(act);
+  const bool fast = DYN == DYN_PHYS || __all(act);
 #if SWARM_DIAG_EXTRA_VALU
   {  // diagnostic: SWARM_DIAG_EXTRA_VALU dependent-free FAST VALU ops per wave
     float z0 = px, z1 = py, z2 = pz, z3 = px + 1.f;
@@ -1615,13 +1659,18 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     if (z0 + z1 + z2 + z3 == 1234.5f) fsum += 1.0;
   }
 #endif
+  if constexpr (DYN == DYN_PHYS) {  // s' keys, no formation; every drone is a contact candidate
+    pair_pass_s64<KS, 2, true>(soa, t, px, py, pz, true, A->P.nb_keep, 0.f, nk, smin, fsum);
+    obstacle_pass_s64<MSL, true>(osoa, M, px, py, pz, true, A->P.s_phys_obst, A->P.ob_keep, ok, ocoll);
+  } else {
 #if SWARM_DIAG_NO_FORMATION
-  if (fast) pair_pass_s64<KS, 0, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
+    if (fast) pair_pass_s64<KS, 0, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
 #else
-  if (fast) pair_pass_s64<KS, 1, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
+    if (fast) pair_pass_s64<KS, 1, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
 #endif
-  else pair_pass_s64<KS, 1, false>(soa, t, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
-  obstacle_pass_s64<MSL, true>(osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
+    else pair_pass_s64<KS, 1, false>(soa, t, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
+    obstacle_pass_s64<MSL, true>(osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
+  }
   if constexpr (LANDED) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next env's inputs are in
   STAMP_AT(env, 3);
   A = s64_args();
@@ -1646,44 +1695,77 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   // [key & keep, key | ~keep] x [FAST_LO, FAST_HI] (truncated d~ within 2^-21 of exact); only
   // a nearest distance inside that band (~1e-5 of the threshold) needs the exact scan.
   bool pcoll;
-  if (fast) {
-    const uint32_t keep = A->P.nb_keep;
-    pcoll = __uint_as_float(nk[0] | ~keep) * FAST_HI <= A->P.thr_pair;
-    if (!pcoll && __uint_as_float(nk[0] & keep) * FAST_LO <= A->P.thr_pair)
-      pcoll = exact_pair_collision(ring, S64_N, t, px, py, pz, A->P.s_pair);
-  } else {
-    pcoll = smin <= A->P.thr_pair * FAST_LO;
-    if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act)
-      pcoll = exact_pair_collision(ring, S64_N, t, px, py, pz, A->P.s_pair);
-  }
-  const float curr = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
-  float rew = 0.f;
+  float curr, rew = 0.f;
   bool reached = false, collided = false;
-  if (act) {
-    reached = (double)curr <= A->P.goal_radius;
-    collided = ocoll || pcoll;
-    double r = ((double)prev_d - (double)curr) * A->P.kp;
-    if (n_active > 1) r = r + (-A->P.kf) * (fsum * inv_count(n_active - 1));
-    if (reached) r = r + A->P.r_goal;
-    if (collided) r = r + A->P.r_col;
-    rew = (float)r;
-  }
-  const bool any_c = __ballot(act && collided) != 0;
-  const bool any_cand = __ballot(act && !reached && !collided) != 0;
   bool term = false, trunc = false, cont = false, term_all = false, trunc_all = false;
   int new_step = stepc;
-  if (n_active == 0) {  // drone_swarm_env.py:93-95
-    term_all = true;
-  } else {
+  if constexpr (DYN == DYN_PHYS) {
+    // drone_physics_env.py:362-419 restated (swarm_kernel, DYN_PHYS): s' keys, every drone a
+    // contact candidate (fast), the nearest key decides against the contact threshold
+    const uint32_t keep = A->P.nb_keep;
+    const float thr = A->P.s_phys_pair;
+    pcoll = __uint_as_float(nk[0] | ~keep) * FAST_HI <= thr;
+    if (!pcoll && __uint_as_float(nk[0] & keep) * FAST_LO <= thr)
+      pcoll = exact_pair_collision(ring, S64_N, t, px, py, pz, thr);
+    const double dx = (double)px - (double)gx;
+    const double dy = (double)py - (double)gy;
+    const double dz = (double)pz - (double)gz;
+    const double dist_phys = dsqrt_rn(((dx * dx) + (dy * dy)) + (dz * dz));
+    curr = (float)dist_phys;
+    collided = ocoll || pcoll || (pz <= A->P.ground_z);
+    reached = dist_phys < A->P.goal_radius;
+    if (act) {
+      double r = (-dist_phys) * 0.1;
+      if (collided) r = r - 10.0;
+      else if (reached) r = r + 50.0;
+      rew = (float)r;
+    }
+    const bool any_c = __ballot(act && collided) != 0;
+    const bool any_notall = __ballot(act && !collided && !reached) != 0;
     new_step = stepc + 1;
     const bool tl = new_step >= A->P.max_steps;
-    term_all = (!any_cand && !any_c && !tl) || any_c;
-    trunc_all = tl && !term_all;
+    const bool done = any_c || !any_notall || tl;
+    trunc_all = done && tl && !any_c && any_notall;
+    term_all = done && !trunc_all;
+    term = term_all;
+    trunc = trunc_all;
+    cont = true;
+  } else {
+    if (fast) {
+      const uint32_t keep = A->P.nb_keep;
+      pcoll = __uint_as_float(nk[0] | ~keep) * FAST_HI <= A->P.thr_pair;
+      if (!pcoll && __uint_as_float(nk[0] & keep) * FAST_LO <= A->P.thr_pair)
+        pcoll = exact_pair_collision(ring, S64_N, t, px, py, pz, A->P.s_pair);
+    } else {
+      pcoll = smin <= A->P.thr_pair * FAST_LO;
+      if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act)
+        pcoll = exact_pair_collision(ring, S64_N, t, px, py, pz, A->P.s_pair);
+    }
+    curr = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
     if (act) {
-      const bool done_i = reached || collided;
-      term = done_i;
-      trunc = tl && !done_i;
-      cont = !done_i && !tl && !any_c;
+      reached = (double)curr <= A->P.goal_radius;
+      collided = ocoll || pcoll;
+      double r = ((double)prev_d - (double)curr) * A->P.kp;
+      if (n_active > 1) r = r + (-A->P.kf) * (fsum * inv_count(n_active - 1));
+      if (reached) r = r + A->P.r_goal;
+      if (collided) r = r + A->P.r_col;
+      rew = (float)r;
+    }
+    const bool any_c = __ballot(act && collided) != 0;
+    const bool any_cand = __ballot(act && !reached && !collided) != 0;
+    if (n_active == 0) {  // drone_swarm_env.py:93-95
+      term_all = true;
+    } else {
+      new_step = stepc + 1;
+      const bool tl = new_step >= A->P.max_steps;
+      term_all = (!any_cand && !any_c && !tl) || any_c;
+      trunc_all = tl && !term_all;
+      if (act) {
+        const bool done_i = reached || collided;
+        term = done_i;
+        trunc = tl && !done_i;
+        cont = !done_i && !tl && !any_c;
+      }
     }
   }
   const bool do_reset = A->P.auto_reset && (term_all || trunc_all) && !(SWARM_ABLATE & ABL_RESET);
@@ -1717,12 +1799,19 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     pz = uni(w[2], lo_w, wd_w);
     vx = vy = vz = 0.f;
     act = true;
-    const float ox = uni(wo[0], lo_w, wd_w), oy = uni(wo[1], lo_w, wd_w), oz = uni(wo[2], lo_w, wd_w);
+    const float ox = uni(wo[0], lo_w, wd_w), oy = uni(wo[1], lo_w, wd_w);
+    float oz = uni(wo[2], lo_w, wd_w), goal_z = oz;
+    if constexpr (DYN == DYN_PHYS) {  // drone_physics_env.py:205-242 ranges (swarm_kernel draw_env)
+      pz = fmaxf(pz, 1.0f);
+      damp = 0.5f * uni(w[3], 0.8f, 0.4f);
+      goal_z = uni(wo[3], 0.5f, 1.5f);
+      oz = fmaxf(oz, 0.5f);
+    }
     wave_sync();  // every read of the old ring / obstacles is done
     if (t < M) s64_put_obst(obst, osoa, t, ox, oy, oz);
     gx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ox), M));
     gy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(oy), M));
-    gz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(oz), M));
+    gz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(goal_z), M));
     s64_put(ring, soa, t, px, py, pz, 1.f);
     wave_sync();
 #pragma unroll
@@ -1736,13 +1825,13 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     obstacle_pass_s64<MSL, false>(osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
     select_topk(false);
   } else {
-    select_topk(true);
+    select_topk(DYN == DYN_KIN);  // the kinematic step pass ranks by d~, physics by s'
   }
 
   STAMP_AT(env, 6);
   A = s64_args();
   // ---- state write-back
-  const bool new_act = do_reset || cont;
+  const bool new_act = do_reset || (DYN == DYN_PHYS ? (act && !(term_all || trunc_all)) : cont);
   float* __restrict__ posE = A->S.pos + ea * 3;
   float* __restrict__ velE = A->S.vel + ea * 3;
   posE[t3] = px; posE[t3 + 1] = py; posE[t3 + 2] = pz;
@@ -1771,6 +1860,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       A->S.goal[3 * env + 0] = gx; A->S.goal[3 * env + 1] = gy; A->S.goal[3 * env + 2] = gz;
     }
   }
+  if (DYN == DYN_PHYS && do_reset) (A->S.damping + ea)[t] = damp;
   if (do_reset && t < M) {
     float* o = A->S.obstacles + ((size_t)env * M) * 3 + t3;
     const float4 q = obst[t];
@@ -1789,6 +1879,15 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   float row[D];
   row[0] = px; row[1] = py; row[2] = pz;
   row[3] = vx; row[4] = vy; row[5] = vz;
+  if constexpr (DYN == DYN_PHYS) {  // the obs velocity is clamped (drone_physics_env.py:438-442)
+    const double dvx = (double)vx, dvy = (double)vy, dvz = (double)vz;
+    const double nv = dsqrt_rn(((dvx * dvx) + (dvy * dvy)) + (dvz * dvz));
+    if (nv > A->P.vmax_d) {
+      row[3] = (float)((dvx / nv) * A->P.vmax_d);
+      row[4] = (float)((dvy / nv) * A->P.vmax_d);
+      row[5] = (float)((dvz / nv) * A->P.vmax_d);
+    }
+  }
   row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
 #pragma unroll
   for (int s = 0; s < S64_K; ++s) {
@@ -1912,10 +2011,9 @@ __device__ __forceinline__ void s64_set_priority() {
 #define SWARM_S64_WG_ENVS 4
 #endif
 constexpr int S64_WG_ENVS = SWARM_S64_WG_ENVS;
-template <int CH, int G>
-__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(8)))
-swarm_step64_once(const S64Args args) {
-  (void)args;  // read through s64_args()
+// The body of both one-wave-per-env kernels (kinematic / physics).
+template <int CH, int G, int DYN>
+__device__ __forceinline__ void s64_once_body() {
   __shared__ S64Lds<CH> lds[G];
   s64_set_priority();
   if constexpr (SWARM_PRIO_MODE >= 2) __builtin_amdgcn_s_setprio(3);  // inputs and integrate first
@@ -1924,9 +2022,25 @@ swarm_step64_once(const S64Args args) {
   const int env = blockIdx.x * G + w;
   if (env >= s64_args()->P.E) return;  // whole wave (the last workgroup of a ragged E)
   S64In cur;
-  s64_load(s64_args(), env, t, cur);
-  s64_env<CH, false>(env, s64_args()->P.M, cur, lds[w].w.ring, lds[w].w.obst,
-                     reinterpret_cast<float*>(lds[w].stage), t, []() {});
+  s64_load<DYN>(s64_args(), env, t, cur);
+  s64_env<CH, false, void (*)(), DYN>(env, s64_args()->P.M, cur, lds[w].w.ring, lds[w].w.obst,
+                                      reinterpret_cast<float*>(lds[w].stage), t, []() {});
+}
+template <int CH, int G>
+__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(8)))
+swarm_step64_once(const S64Args args) {
+  (void)args;  // read through s64_args()
+  s64_once_body<CH, G, DYN_KIN>();
+}
+// The physics restatement (DronePhysicsEnv, point mass) at the same shape: the
+// same rings, passes, finish and obs staging, with the substep integrate, s' keys, contact
+// thresholds, physics rewards / terminations, reset ranges and the clamped obs velocity of
+// swarm_kernel<0, DYN_PHYS, 4, 5, 2>, bit for bit.
+template <int CH, int G>
+__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(8)))
+swarm_step64_phys_once(const S64Args args) {
+  (void)args;
+  s64_once_body<CH, G, DYN_PHYS>();
 }
 
 template <int CH>
@@ -2037,9 +2151,10 @@ SWARM_PICK_DECL(1);
 SWARM_PICK_DECL(2);
 SWARM_PICK_DECL(3);
 // the headline specialisation (SWARM_PART 5)
-__attribute__((visibility("hidden"))) void* swarm_pick_step64(bool persistent);
+__attribute__((visibility("hidden"))) void* swarm_pick_step64(bool persistent, bool physics);
 #if SWARM_HAS_PART(5)
-__attribute__((visibility("hidden"))) void* swarm_pick_step64(bool persistent) {
+__attribute__((visibility("hidden"))) void* swarm_pick_step64(bool persistent, bool physics) {
+  if (physics) return reinterpret_cast<void*>(swarm_step64_phys_once<S64_CH, S64_WG_ENVS>);
   return persistent ? reinterpret_cast<void*>(swarm_step64<S64_CH>)
                     : reinterpret_cast<void*>(swarm_step64_once<S64_CH, S64_WG_ENVS>);
 }
@@ -2117,7 +2232,7 @@ int obs_dim_of(const swarm_params_t* p) {
 // kinematic/swarm mode (buffer alignment is checked at launch).
 bool step64_applies(const swarm_params_t* p, const KParams& k) {
   return p->kernel_path == SWARM_PATH_AUTO && k.N == S64_N && k.K == S64_K && k.Ms == S64_MS && k.M >= S64_MS &&
-         k.M <= S64_MMAX && p->dynamics == DYN_KIN;
+         k.M <= S64_MMAX && (p->dynamics == DYN_KIN || p->dynamics == DYN_PHYS);
 }
 
 // Persistent grid of swarm_step64: waves_per_simd x 4 SIMDs x the current device's CUs (E when
@@ -2275,14 +2390,15 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
                                                        (uintptr_t)s->active) % 4 == 0) ? 1 : 0;
   if (mode == MODE_STEP && step64_applies(p, kp) && kp.obs_vec4 && kp.pack_bytes && !s->env_cfg) {
     swarm_state_t st = *s;
-    const int grid = step64_grid(p, kp.E);
+    const bool phys = p->dynamics == DYN_PHYS;  // physics: the one-wave-per-env launch only
+    const int grid = phys ? kp.E : step64_grid(p, kp.E);
     if (grid >= kp.E) st.work = nullptr;  // one env per workgroup: nothing to dequeue
     const S64Args args{kp, st, actions, amask, *o};
     if (st.work)
-      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step64(true)), dim3(grid), dim3(64), 0,
+      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step64(true, false)), dim3(grid), dim3(64), 0,
                          (hipStream_t)stream, args);
     else
-      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step64(false)),
+      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step64(false, phys)),
                          dim3((kp.E + S64_WG_ENVS - 1) / S64_WG_ENVS), dim3(64 * S64_WG_ENVS), 0, (hipStream_t)stream,
                          args);
     hipError_t e = hipGetLastError();
@@ -2421,7 +2537,7 @@ int swarm_query_launch(const swarm_params_t* p, swarm_launch_info_t* info) {
   if (!info) return fail(SWARM_ENULL, "info is NULL");
   const int rc = build_kparams(p, &kp, info);
   if (rc == SWARM_OK && step64_applies(p, kp)) {  // geometry of the step launch (reset/observe stay generic)
-    const int grid = step64_grid(p, kp.E);
+    const int grid = p->dynamics == DYN_PHYS ? kp.E : step64_grid(p, kp.E);
     const int lds_env = (int)sizeof(S64Lds<S64_CH>);
     info->lanes_per_env = 64;
     if (grid < kp.E) {  // persistent grid with env queues (launched when state.work is given)

@@ -440,7 +440,7 @@ class VecSwarm:
 
     def kernel_name(self) -> str:
         """Kernel the step launches: the headline specialisation swarm_step64_once<32, 4> (one
-        wave per env, 4 per workgroup) or its persistent form swarm_step64<32> (E larger than
+        wave per env, 4 per workgroup; swarm_step64_phys_once<32, 4> in physics mode) or its persistent form swarm_step64<32> (E larger than
         the resident grid, env queues in `work`), else the generic swarm_kernel<KIND, DYN, KS,
         MSL, LM> (KIND 0 = step; LM lane mode 0 block / 1 multi-team wave / 2 one team per wave).
         With env groups: the kernel of group 0."""
@@ -451,7 +451,7 @@ class VecSwarm:
         if kid == nat.KERNEL_STEP64_PERSISTENT and self.persistent:
             return "swarm_step64<32>"
         if kid in (nat.KERNEL_STEP64, nat.KERNEL_STEP64_PERSISTENT):
-            return "swarm_step64_once<32, 4>"
+            return "swarm_step64_phys_once<32, 4>" if self.dynamics == "physics" else "swarm_step64_once<32, 4>"
         lanes = int(li.lanes_per_env)
         lm = 0 if lanes > 64 else (2 if lanes == 64 else 1)
         return (f"swarm_kernel<0, {int(self.params.dynamics)}, {int(li.neighbor_slots)}, "

@@ -57,7 +57,10 @@ def test_kernel_selection():
         v = VecSwarm(4, raw, device=d)
         assert int(v.launch_info.kernel_id) == nat.KERNEL_GENERIC, raw
     v = VecSwarm(4, {"num_drones": 64}, device=d, dynamics="physics")
-    assert int(v.launch_info.kernel_id) == nat.KERNEL_GENERIC
+    assert int(v.launch_info.kernel_id) == nat.KERNEL_STEP64
+    assert v.kernel_name() == "swarm_step64_phys_once<32, 4>"
+    v = VecSwarm(4, {"num_drones": 64}, device=d, dynamics="physics", waves_per_simd=4)
+    assert int(v.launch_info.kernel_id) == nat.KERNEL_STEP64  # physics: one wave per env only
     v = VecSwarm(4, {"num_drones": 64}, device=d, kernel_path="generic")
     assert v.kernel_name().startswith("swarm_kernel<0, 0, 4, 5, 2>")
 
@@ -177,3 +180,53 @@ def test_step64_persistent_queue_matches_generic(dev, wps, e):
         b.step(act)
         _assert_same(a, b, f"persistent wps={wps} t={t}")
         assert int(torch.count_nonzero(a.work)) == 0, "queue heads not reset"
+
+
+@pytest.mark.parametrize("m,max_steps,masked,law", [(8, 9, False, 0), (8, 400, True, 0), (4, 6, False, 1),
+                                                    (16, 12, True, 1), (11, 5, False, 0)])
+def test_step64_physics_matches_generic(dev, m, max_steps, masked, law):
+    """swarm_step64_phys_once vs swarm_kernel<0, 1, 4, 5, 2>: bit-identical outputs and state
+    (damping included) over steps with auto-resets, both damping laws, with / without masks."""
+    raw = dict(num_drones=64, num_obstacles=m, max_steps=max_steps)
+    e = 2048
+    a, b = _pair(dev, raw, e, auto_reset=True, seed=9, env_offset=5, dynamics="physics",
+                 physics={"damping_law": law})
+    assert a.kernel_name() == "swarm_step64_phys_once<32, 4>"
+    assert b.kernel_name().startswith("swarm_kernel<0, 1, 4, 5, 2>")
+    a.reset()
+    b.reset()
+    _assert_same(a, b, "reset")
+    g = torch.Generator(device=dev).manual_seed(91 + m)
+    resets = 0
+    for t in range(14):
+        act = torch.rand((e, 64, 3), device=dev, generator=g) * 3.0 - 1.5
+        am = (torch.rand((e, 64), device=dev, generator=g) > 0.1) if masked else None
+        a.step(act, am)
+        b.step(act, am)
+        _assert_same(a, b, f"physics t={t}")
+        assert torch.equal(a.damping, b.damping), f"physics t={t}: damping"
+        resets += int(((a.env_done & 4) != 0).sum())
+    assert resets > 0
+
+
+def test_step64_physics_vs_oracle(dev):
+    """A 32-env slice of the physics step64 batch against the oracle's point-mass restatement."""
+    from oracle import swarm_oracle as so
+    from swarm_marl_amd import VecSwarm
+    raw = dict(num_drones=64, num_obstacles=8, max_steps=7)
+    cfg = oracle_cfg(raw)
+    e = 32
+    v = VecSwarm(e, raw, device=dev, auto_reset=True, seed=13, dynamics="physics", with_infos=True,
+                 with_global_state=True)
+    assert v.kernel_name() == "swarm_step64_phys_once<32, 4>"
+    v.reset()
+    g = torch.Generator(device=dev).manual_seed(5)
+    for t in range(9):
+        st = vec_state_numpy(v)
+        act = torch.rand((e, 64, 3), device=dev, generator=g) * 2 - 1
+        v.step(act)
+        ns, out = so.step(cfg, st, act.cpu().numpy(), physics=True, auto_reset=True, seed=13)
+        assert np.array_equal(v.obs.cpu().numpy(), out["obs"]), f"t={t} obs"
+        assert np.abs(v.reward.cpu().numpy().astype(np.float64) - out["reward"]).max() < 1e-5, f"t={t}"
+        for k in ("pos", "vel", "goal", "obst", "active", "step", "episode", "damping"):
+            assert np.array_equal(vec_state_numpy(v)[k], ns[k]), f"t={t} {k}"
