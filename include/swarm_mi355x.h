@@ -318,6 +318,9 @@ typedef struct swarm_eval {
                              rest are dropped) */
   int32_t capacity;       /* a multiple of SWARM_EVAL_SEGMENTS */
   int32_t update_index;   /* stamped into the records this update closes (the caller counts updates) */
+  const float* state_pos;   /* [E,N,3] optional: the env state's positions after the step (bitwise
+                               obs[..., 0:3]), read contiguously instead of from the obs rows */
+  const float* state_goal;  /* [E,3] optional (with state_pos): the goal; obs[..., 6:9] = goal - pos */
 } swarm_eval_t;
 
 /* Start an episode in the masked envs (all if NULL) from the current obs (after a reset). */

@@ -30,7 +30,9 @@
 
 namespace {
 
-constexpr int EVAL_THREADS = 64;
+constexpr int EVAL_THREADS = 64;   // one wave per env
+constexpr int EVAL_WG_ENVS = 4;    // independent waves per workgroup: a quarter of the workgroups
+                                   // to dispatch (8192 one-wave workgroups cost the dispatcher ~4 us)
 #ifndef SWARM_EVAL_ABLATE  // diagnostics (tools/): 1 = skip the formation error, 2 = skip episode
 #define SWARM_EVAL_ABLATE 0  // ends, 3 = no counter atomic (slot 0 of the segment), 4 = 1 + 2, 5 = return
 #endif                       // after the first loads
@@ -79,14 +81,35 @@ struct EvalArgs {
 };
 
 // Episode start of env e from its current observation rows (every agent).
+// obs[0:3] and obs[6:9] of row r (agent i of env e): from the state (contiguous; bitwise the
+// same floats: the step writes px and gx - px) when given, else from the obs row
+__device__ __forceinline__ void obs_pos(const EvalArgs& a, size_t r, float& x, float& y, float& z) {
+  if (a.ev.state_pos) {
+    x = a.ev.state_pos[3 * r]; y = a.ev.state_pos[3 * r + 1]; z = a.ev.state_pos[3 * r + 2];
+  } else {
+    const float* o = a.obs + r * a.D;
+    x = o[0]; y = o[1]; z = o[2];
+  }
+}
+__device__ __forceinline__ void obs_goal_vec(const EvalArgs& a, int e, size_t r, float px, float py, float pz,
+                                             float& x, float& y, float& z) {
+  if (a.ev.state_pos) {
+    x = a.ev.state_goal[3 * e] - px; y = a.ev.state_goal[3 * e + 1] - py; z = a.ev.state_goal[3 * e + 2] - pz;
+  } else {
+    const float* o = a.obs + r * a.D;
+    x = o[6]; y = o[7]; z = o[8];
+  }
+}
+
 __device__ void begin_env(const EvalArgs& a, int e, int t) {
   const swarm_eval_t& v = a.ev;
   for (int i = t; i < a.N; i += EVAL_THREADS) {
     const size_t r = (size_t)e * a.N + i;
-    const float* o = a.obs + r * a.D;
-    const float px = o[0], py = o[1], pz = o[2];
+    float px, py, pz, rx, ry, rz;
+    obs_pos(a, r, px, py, pz);
+    obs_goal_vec(a, e, r, px, py, pz, rx, ry, rz);
     v.start[3 * r] = px; v.start[3 * r + 1] = py; v.start[3 * r + 2] = pz;
-    v.goal[3 * r] = px + o[6]; v.goal[3 * r + 1] = py + o[7]; v.goal[3 * r + 2] = pz + o[8];
+    v.goal[3 * r] = px + rx; v.goal[3 * r + 1] = py + ry; v.goal[3 * r + 2] = pz + rz;
     v.last[3 * r] = px; v.last[3 * r + 1] = py; v.last[3 * r + 2] = pz;
     v.traveled[r] = 0.0;
   }
@@ -99,10 +122,10 @@ __device__ void begin_env(const EvalArgs& a, int e, int t) {
   }
 }
 
-__global__ void __launch_bounds__(EVAL_THREADS) eval_begin_kernel(const EvalArgs a) {
-  const int e = blockIdx.x;
-  if (a.env_mask && !a.env_mask[e]) return;
-  begin_env(a, e, threadIdx.x);
+__global__ void __launch_bounds__(EVAL_THREADS * EVAL_WG_ENVS) eval_begin_kernel(const EvalArgs a) {
+  const int e = blockIdx.x * EVAL_WG_ENVS + (threadIdx.x >> 6);
+  if (e >= a.E || (a.env_mask && !a.env_mask[e])) return;
+  begin_env(a, e, threadIdx.x & 63);
 }
 
 // One wave per env.  Every global load of the step is issued in one batch at the top (the env's
@@ -111,12 +134,15 @@ __global__ void __launch_bounds__(EVAL_THREADS) eval_begin_kernel(const EvalArgs
 // the goal columns of a restarting one): the kernel is latency-bound (all 8192 waves of the
 // headline batch are resident at once), so the chain of dependent memory round trips, not the
 // bytes, sets its time.  A restart writes the new episode's start rows in the same pass.
-__global__ void __launch_bounds__(EVAL_THREADS) eval_update_kernel(const EvalArgs a) {
+__global__ void __launch_bounds__(EVAL_THREADS * EVAL_WG_ENVS) eval_update_kernel(const EvalArgs a) {
   // agents with an observation this step (x, y, z, has); N float4 of dynamic LDS, so that the
   // LDS of a small swarm does not cap the waves per CU (a static EVAL_MAX_N array did: 16 KB)
-  extern __shared__ float4 pos[];
-  const int e = blockIdx.x;
-  const int t = threadIdx.x;
+  extern __shared__ float4 pos_all[];
+  const int w = threadIdx.x >> 6;
+  const int e = blockIdx.x * EVAL_WG_ENVS + w;
+  const int t = threadIdx.x & 63;
+  if (e >= a.E) return;  // whole wave
+  float4* pos = pos_all + (size_t)w * a.N;  // this wave's slice: waves never share LDS
   const swarm_eval_t& v = a.ev;
   const uint8_t status = v.status[e];  // uniform
   const uint8_t done = a.env_done[e];
@@ -134,10 +160,10 @@ __global__ void __launch_bounds__(EVAL_THREADS) eval_update_kernel(const EvalArg
   int n_st = 0, n_obs = 0, coll = 0, not_reached = 0;
   for (int i = t; i < a.N; i += EVAL_THREADS) {
     const size_t r = (size_t)e * a.N + i;
-    const float* o = a.obs + r * a.D;
     const uint8_t fl = a.info_flags[r];
     const float rw = a.reward[r];
-    const float ox = o[0], oy = o[1], oz = o[2];
+    float ox, oy, oz;
+    obs_pos(a, r, ox, oy, oz);
     const float lx = v.last[3 * r], ly = v.last[3 * r + 1], lz = v.last[3 * r + 2];
     double tr = v.traveled[r];
     float sx = 0.f, sy = 0.f, sz = 0.f, gx = 0.f, gy = 0.f, gz = 0.f, rx = 0.f, ry = 0.f, rz = 0.f;
@@ -145,7 +171,7 @@ __global__ void __launch_bounds__(EVAL_THREADS) eval_update_kernel(const EvalArg
       sx = v.start[3 * r]; sy = v.start[3 * r + 1]; sz = v.start[3 * r + 2];
       gx = v.goal[3 * r]; gy = v.goal[3 * r + 1]; gz = v.goal[3 * r + 2];
     }
-    if (restarts) { rx = o[6]; ry = o[7]; rz = o[8]; }
+    if (restarts) obs_goal_vec(a, e, r, ox, oy, oz, rx, ry, rz);
     if (fl & SWARM_AGENT_STEPPED) {
       rsum += (double)rw;
       ++n_st;
@@ -174,7 +200,10 @@ __global__ void __launch_bounds__(EVAL_THREADS) eval_update_kernel(const EvalArg
       v.last[3 * r] = ox; v.last[3 * r + 1] = oy; v.last[3 * r + 2] = oz;
     }
   }
-  __syncthreads();
+  // LDS ordering within one wave: a compiler fence around the wave barrier suffices
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   rsum = wave_sum(rsum);
   n_st = wave_sum_i(n_st);
   n_obs = wave_sum_i(n_obs);
@@ -275,6 +304,8 @@ int make_args(const swarm_params_t* p, const swarm_eval_t* ev, const swarm_out_t
   if (!ev->ep_reward || !ev->ep_steps || !ev->reached_step || !ev->status || !ev->fe_sum || !ev->start || !ev->goal ||
       !ev->last || !ev->traveled || !ev->records || !ev->count)
     return efail(SWARM_ENULL, "an eval state buffer is NULL");
+  if ((ev->state_pos == nullptr) != (ev->state_goal == nullptr))
+    return efail(SWARM_EINVAL, "state_pos and state_goal go together");
   if (ev->capacity < 0 || ev->capacity % SWARM_EVAL_SEGMENTS != 0)
     return efail(SWARM_EINVAL, "capacity must be a non-negative multiple of %d", SWARM_EVAL_SEGMENTS);
   a->E = p->num_envs;
@@ -302,7 +333,8 @@ int swarm_eval_begin(const swarm_params_t* p, const swarm_eval_t* ev, const swar
   if (rc) return rc;
   if (a.E == 0) return SWARM_OK;
   a.env_mask = env_mask;
-  hipLaunchKernelGGL(eval_begin_kernel, dim3(a.E), dim3(EVAL_THREADS), 0, (hipStream_t)hip_stream, a);
+  hipLaunchKernelGGL(eval_begin_kernel, dim3((a.E + EVAL_WG_ENVS - 1) / EVAL_WG_ENVS), dim3(EVAL_THREADS * EVAL_WG_ENVS),
+                     0, (hipStream_t)hip_stream, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? SWARM_OK : efail(SWARM_EHIP, "eval_begin launch: %s", hipGetErrorString(e));
 }
@@ -314,7 +346,8 @@ int swarm_eval_update(const swarm_params_t* p, const swarm_eval_t* ev, const swa
   if (!o->reward || !o->info_flags || !o->env_done)
     return efail(SWARM_ENULL, "out.reward/info_flags/env_done required (build the env with infos)");
   if (a.E == 0) return SWARM_OK;
-  hipLaunchKernelGGL(eval_update_kernel, dim3(a.E), dim3(EVAL_THREADS), (unsigned)(a.N * sizeof(float4)),
+  hipLaunchKernelGGL(eval_update_kernel, dim3((a.E + EVAL_WG_ENVS - 1) / EVAL_WG_ENVS), dim3(EVAL_THREADS * EVAL_WG_ENVS),
+                     (unsigned)(EVAL_WG_ENVS * a.N * sizeof(float4)),
                      (hipStream_t)hip_stream, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? SWARM_OK : efail(SWARM_EHIP, "eval_update launch: %s", hipGetErrorString(e));

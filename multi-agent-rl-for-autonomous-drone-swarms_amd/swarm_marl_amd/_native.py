@@ -144,7 +144,8 @@ class SwarmPolicy(ctypes.Structure):
 class SwarmEval(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name in
                 ("ep_reward", "ep_steps", "reached_step", "status", "fe_sum", "start", "goal", "last",
-                 "traveled", "records", "count")] + [("capacity", ctypes.c_int32), ("update_index", ctypes.c_int32)]
+                 "traveled", "records", "count")] + [("capacity", ctypes.c_int32), ("update_index", ctypes.c_int32),
+                                                     ("state_pos", ctypes.c_void_p), ("state_goal", ctypes.c_void_p)]
 
 
 class SwarmLaunchInfo(ctypes.Structure):

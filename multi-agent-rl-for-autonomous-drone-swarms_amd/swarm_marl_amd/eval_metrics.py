@@ -83,6 +83,8 @@ class EvalTracker:
             setattr(c, name, getattr(self, name).data_ptr())
         c.records = self.records_buf.data_ptr()
         c.capacity = self.capacity
+        # positions / goal from the state tensors (contiguous) rather than the strided obs rows
+        c.state_pos, c.state_goal = vec.pos.data_ptr(), vec.goal.data_ptr()
         self._c = c
 
     def _stream(self) -> int:
@@ -118,6 +120,9 @@ class EvalTracker:
             setattr(c, name, t.data_ptr() + lo * t.stride(0) * t.element_size())
         c.records, c.count, c.capacity = self.records_buf.data_ptr(), self.count.data_ptr(), self.capacity
         c.update_index = self.updates
+        v = self.vec
+        c.state_pos = v.pos.data_ptr() + lo * v.pos.stride(0) * v.pos.element_size()
+        c.state_goal = v.goal.data_ptr() + lo * v.goal.stride(0) * v.goal.element_size()
         return c
 
     def records(self) -> np.ndarray:
