@@ -129,6 +129,8 @@ def max_over_ranks(values, world: int, device=None) -> list[float]:
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
     if world > 1:
         import torch.distributed as dist
+        if dist.get_backend() == "gloo":  # rehearsal backend: host tensors
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in t.cpu()]
 
@@ -249,10 +251,16 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # SWARM_BENCH_REHEARSAL=1: every rank on cuda:0 with the gloo backend — the multi-rank code
+    # path (sharding, barriers, max-reduce) rehearsed on a one-GPU box; not a scaling measurement
+    rehearsal = os.environ.get("SWARM_BENCH_REHEARSAL") == "1"
+    if rehearsal and args.ctde:
+        raise SystemExit("SWARM_BENCH_REHEARSAL runs without --ctde (the gather needs RCCL)")
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local if world > 1 else 0)
+        if not rehearsal:
+            torch.cuda.set_device(local)
+        dist.init_process_group("gloo" if rehearsal else "nccl")
+    dev = torch.device("cuda", local if world > 1 and not rehearsal else 0)
     torch.cuda.set_device(dev)
 
     from swarm_marl_amd import VecSwarm
@@ -525,6 +533,8 @@ def main(argv=None):
                        "ctde_gather_every": args.gather_every if gather_buf is not None else None},
             "roofline": roof,
             "env_done_fraction_last_step": done_frac,
+            **({"rehearsal": f"{world} ranks sharing cuda:0 over gloo (SWARM_BENCH_REHEARSAL): the "
+                             "multi-rank code path, not a scaling measurement"} if rehearsal else {}),
         }
         if pol is not None:
             rows = e * n
