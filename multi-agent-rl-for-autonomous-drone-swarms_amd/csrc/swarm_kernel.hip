@@ -601,6 +601,16 @@ __device__ __forceinline__ void exact_select(const float4* __restrict__ pts, int
   }
 }
 
+// A nearest key whose value bits are 0 decides the band without the exact scan (coincident
+// drones, e.g. stacked in a world-clip corner).  d~ keys (DKEY): v_sqrt_f32 of a nonzero s'
+// (denormals are kept in this code) is >= 2^-75, so value bits 0 mean s' = 0, i.e. every f32
+// square rounds to 0, i.e. the sdot sum is 0: within any threshold >= 0.  s' keys: value bits 0
+// mean s' < 2^-143, and the exact sum is then below FLT_MIN: within any threshold >= FLT_MIN.
+template <bool DKEY>
+__device__ __forceinline__ bool key_zero_hit(uint32_t key, uint32_t keep, float s_thr) {
+  return (key & keep) == 0u && s_thr >= (DKEY ? 0.f : 0x1p-126f);
+}
+
 // exact "any eligible pair within s_thr" (fallback of the banded running minimum); the f32 sum
 // filters, the sdot-exact sum decides
 __device__ __forceinline__ bool exact_pair_collision(const float4* __restrict__ pts, int count, int self,
@@ -953,7 +963,8 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         const float thr = (DYN == DYN_KIN) ? d_thr : s_exact_thr;
         pcoll = __uint_as_float(nk[0] | ~P.nb_keep) * FAST_HI <= thr;
         if (!pcoll && __uint_as_float(nk[0] & P.nb_keep) * FAST_LO <= thr)
-          pcoll = exact_pair_collision(ring, N, t, px, py, pz, s_exact_thr);
+          pcoll = key_zero_hit<DYN == DYN_KIN>(nk[0], P.nb_keep, s_exact_thr) ||
+                  exact_pair_collision(ring, N, t, px, py, pz, s_exact_thr);
       } else {
         // smin holds d~ (kinematic) or s' (physics): certain below the band, exact inside it
         const float band_thr = (DYN == DYN_KIN) ? d_thr : s_exact_thr;
@@ -1706,7 +1717,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     const float thr = A->P.s_phys_pair;
     pcoll = __uint_as_float(nk[0] | ~keep) * FAST_HI <= thr;
     if (!pcoll && __uint_as_float(nk[0] & keep) * FAST_LO <= thr)
-      pcoll = exact_pair_collision(ring, S64_N, t, px, py, pz, thr);
+      pcoll = key_zero_hit<false>(nk[0], keep, thr) || exact_pair_collision(ring, S64_N, t, px, py, pz, thr);
     const double dx = (double)px - (double)gx;
     const double dy = (double)py - (double)gy;
     const double dz = (double)pz - (double)gz;
@@ -1735,7 +1746,8 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       const uint32_t keep = A->P.nb_keep;
       pcoll = __uint_as_float(nk[0] | ~keep) * FAST_HI <= A->P.thr_pair;
       if (!pcoll && __uint_as_float(nk[0] & keep) * FAST_LO <= A->P.thr_pair)
-        pcoll = exact_pair_collision(ring, S64_N, t, px, py, pz, A->P.s_pair);
+        pcoll = key_zero_hit<true>(nk[0], keep, A->P.s_pair) ||
+                exact_pair_collision(ring, S64_N, t, px, py, pz, A->P.s_pair);
     } else {
       pcoll = smin <= A->P.thr_pair * FAST_LO;
       if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act)

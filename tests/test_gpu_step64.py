@@ -230,3 +230,37 @@ def test_step64_physics_vs_oracle(dev):
         assert np.abs(v.reward.cpu().numpy().astype(np.float64) - out["reward"]).max() < 1e-5, f"t={t}"
         for k in ("pos", "vel", "goal", "obst", "active", "step", "episode", "damping"):
             assert np.array_equal(vec_state_numpy(v)[k], ns[k]), f"t={t} {k}"
+
+
+@pytest.mark.parametrize("radius,dyn", [(0.0, "kinematic"), (0.5, "kinematic"), (0.0, "physics")])
+@pytest.mark.parametrize("path", ["auto", "generic"])
+def test_coincident_drones_vs_oracle(dev, radius, dyn, path):
+    """Drones stacked on a few points (world-clip corners): nearest keys of value 0 decide the
+    pair contact without the exact scan; obs (exact ties ordered by index), rewards and flags as
+    the oracle, with zero and default radii."""
+    from oracle import swarm_oracle as so
+    from swarm_marl_amd import VecSwarm
+    raw = dict(num_drones=64, collision_radius=radius, goal_radius=radius, max_steps=50)
+    cfg = oracle_cfg(raw)
+    e = 24
+    v = VecSwarm(e, raw, device=dev, auto_reset=True, seed=3, dynamics=dyn, kernel_path=path)
+    v.reset()
+    st = vec_state_numpy(v)
+    rng = np.random.default_rng(11)
+    corners = np.array([[10, 10, 10], [-10, 10, 10], [10, -10, -10], [3.25, -1.5, 2.0]], np.float32)
+    pos = st["pos"].copy()
+    for k in range(e):
+        ncorner = 1 + k % 4
+        pos[k] = corners[rng.integers(0, ncorner, 64)]
+        pos[k, : k % 7] += rng.uniform(-3, 3, (k % 7, 3)).astype(np.float32)
+    v.set_state(pos=pos, vel=np.zeros_like(pos), active=np.ones((e, 64), bool),
+                step_count=np.zeros(e, np.int32))
+    for t in range(3):
+        st = vec_state_numpy(v)
+        act = np.zeros((e, 64, 3), np.float32) if t == 0 else rng.uniform(-1, 1, (e, 64, 3)).astype(np.float32)
+        v.step(torch.as_tensor(act, device=dev))
+        ns, out = so.step(cfg, st, act, physics=dyn == "physics", auto_reset=True, seed=3)
+        assert np.array_equal(v.obs.cpu().numpy(), out["obs"]), f"t={t} obs"
+        assert np.abs(v.reward.cpu().numpy().astype(np.float64) - out["reward"]).max() < 1e-5, f"t={t}"
+        assert np.array_equal(v.terminated.cpu().numpy(), out["terminated"]), f"t={t}"
+        assert np.array_equal(vec_state_numpy(v)["pos"], ns["pos"]), f"t={t}"
