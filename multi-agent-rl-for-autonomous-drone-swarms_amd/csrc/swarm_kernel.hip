@@ -29,6 +29,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <atomic>
@@ -102,6 +103,7 @@ struct KParams {
   int log2_lanes, envs_per_block, chunk_rows, obs_vec4, pack_bytes;
   int off_obst, off_stage, obst_stride, ring;   // ring: pos4 slots per team (2L wave, L block)
   int off_pair;   // block teams with N a power of two: pair-entry ring (BLK_PAIR_STRIDE floats x 2N)
+  int obs_direct;  // multi-team wave kernels: obs rows stored from registers (no LDS staging)
   uint32_t nb_keep, ob_keep;        // key masks: high bits kept from the distance, low bits = index
   long long env_offset;
   unsigned seed_lo, seed_hi;
@@ -1217,8 +1219,9 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   };
 
   if (SWARM_ABLATE & ABL_OBS) {
-  } else if (mode != MODE_STEP && env_mask != nullptr) {
-    // masked reset/observe: rows straight to global memory (off the hot path)
+  } else if ((mode != MODE_STEP && env_mask != nullptr) || (LM == 1 && P.obs_direct)) {
+    // masked reset/observe (off the hot path), and small multi-team launches (latency-bound: the
+    // LDS round trip and barriers of the staging lengthen every wave): rows straight to memory
     if (is_agent && sel) write_row(O.obs + (size_t)ag * D);
   } else {
     // chunks of CH rows staged in LDS, then 16-B coalesced stores of the contiguous block region
@@ -2329,6 +2332,16 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   const long long lds = k.off_stage + (long long)ch * row_bytes;
   if (lds > LDS_LIMIT) return fail(SWARM_ELIMIT, "LDS footprint %lld B exceeds %d B (N=%d, M=%d)", lds, LDS_LIMIT, k.N, k.M);
   k.obs_vec4 = (((long long)rows * k.D) % 4 == 0 && ((long long)ch * k.D) % 4 == 0) ? 1 : 0;
+  // Small multi-team wave launches (<= 2048 one-wave workgroups, two per SIMD) are latency-bound:
+  // rows go straight from registers to memory (N=16: E=1024 14.0 -> 13.1 us per step, E=8192
+  // 18.4 -> 18.2); larger ones keep the coalescing LDS stage (E=32768: 33.1 vs 42.7 us direct).
+  // SWARM_OBS_DIRECT=0/1 overrides (diagnostics).
+  {
+    const long long blocks = ((long long)k.E + G - 1) / G;
+    k.obs_direct = (wave && lanes < 64 && blocks <= 2048) ? 1 : 0;
+    const char* ov = getenv("SWARM_OBS_DIRECT");
+    if (ov && (ov[0] == '0' || ov[0] == '1')) k.obs_direct = ov[0] == '1';
+  }
   // neighbour keys carry the drone index (block) or the rotation offset in [1, L) (wave)
   const int nb_bits = k.log2_lanes;
   const int ob_bits = ilog2(k.M > 1 ? k.M : 2);
