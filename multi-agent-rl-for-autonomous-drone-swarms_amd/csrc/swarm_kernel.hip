@@ -1219,7 +1219,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   };
 
   if (SWARM_ABLATE & ABL_OBS) {
-  } else if ((mode != MODE_STEP && env_mask != nullptr) || (LM == 1 && P.obs_direct)) {
+  } else if ((mode != MODE_STEP && env_mask != nullptr) || (LM != 2 && P.obs_direct)) {
     // masked reset/observe (off the hot path), and small multi-team launches (latency-bound: the
     // LDS round trip and barriers of the staging lengthen every wave): rows straight to memory
     if (is_agent && sel) write_row(O.obs + (size_t)ag * D);
@@ -2332,13 +2332,14 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
   const long long lds = k.off_stage + (long long)ch * row_bytes;
   if (lds > LDS_LIMIT) return fail(SWARM_ELIMIT, "LDS footprint %lld B exceeds %d B (N=%d, M=%d)", lds, LDS_LIMIT, k.N, k.M);
   k.obs_vec4 = (((long long)rows * k.D) % 4 == 0 && ((long long)ch * k.D) % 4 == 0) ? 1 : 0;
-  // Small multi-team wave launches (<= 2048 one-wave workgroups, two per SIMD) are latency-bound:
-  // rows go straight from registers to memory (N=16: E=1024 14.0 -> 13.1 us per step, E=8192
-  // 18.4 -> 18.2); larger ones keep the coalescing LDS stage (E=32768: 33.1 vs 42.7 us direct).
+  // Small launches of multi-team waves or block teams (<= 2048 workgroups) are latency-bound: rows
+  // go straight from registers to memory (N=16: E=1024 14.0 -> 13.1 us per step, E=8192 18.4 ->
+  // 18.2; N=256 x E=1024 in 2 groups 63.0 -> 60.6); larger ones keep the coalescing LDS stage
+  // (N=16, E=32768: 33.1 vs 42.7 us direct).  One-env waves (lanes = 64) always stage.
   // SWARM_OBS_DIRECT=0/1 overrides (diagnostics).
   {
     const long long blocks = ((long long)k.E + G - 1) / G;
-    k.obs_direct = (wave && lanes < 64 && blocks <= 2048) ? 1 : 0;
+    k.obs_direct = (lanes != 64 && blocks <= 2048) ? 1 : 0;
     const char* ov = getenv("SWARM_OBS_DIRECT");
     if (ov && (ov[0] == '0' || ov[0] == '1')) k.obs_direct = ov[0] == '1';
   }
