@@ -20,6 +20,7 @@ if sys.argv[1] == "build":
                     "-I", str(ROOT / "include"), "-DSWARM_STAMPS", "-DSWARM_DEV_HOT", *sys.argv[2:],
                     str(ROOT / "multi-agent-rl-for-autonomous-drone-swarms_amd/csrc/swarm_kernel.hip"),
                     str(ROOT / "multi-agent-rl-for-autonomous-drone-swarms_amd/csrc/swarm_policy.hip"),
+                    str(ROOT / "multi-agent-rl-for-autonomous-drone-swarms_amd/csrc/swarm_eval.hip"),
                     "-o", str(LIB)], check=True)
     sys.exit(0)
 
