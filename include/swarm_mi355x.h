@@ -202,7 +202,8 @@ typedef struct swarm_launch_info {
   int32_t neighbor_slots;   /* compile-time top-K slots of the chosen kernel variant */
   int32_t obstacle_slots;
   int32_t obs_dim;
-  int32_t staged_obs;       /* 1: obs staged through LDS and stored coalesced */
+  int32_t staged_obs;       /* 1: obs staged through LDS and stored coalesced; 0: rows stored from
+                               registers (small latency-bound launches, lanes_per_env != 64) */
   int32_t kernel_id;        /* SWARM_KERNEL_* swarm_step launches for these params (aligned buffers) */
 } swarm_launch_info_t;
 

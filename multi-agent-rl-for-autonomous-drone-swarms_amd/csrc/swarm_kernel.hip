@@ -2385,7 +2385,7 @@ int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* inf
     info->neighbor_slots = neighbor_slots(k.K);
     info->obstacle_slots = obstacle_slots(k.Ms, k.M);
     info->obs_dim = k.D;
-    info->staged_obs = 1;
+    info->staged_obs = k.obs_direct ? 0 : 1;
     info->kernel_id = SWARM_KERNEL_GENERIC;
   }
   return SWARM_OK;

@@ -95,6 +95,17 @@ def test_launch_geometry(nat, lib, n):
     assert 0 < info.lds_bytes <= 160 * 1024
     assert info.neighbor_slots == 4 and info.obstacle_slots == 5  # K=3 -> 4 keys, Ms=4 -> 5
     assert info.obs_dim == 37
+    # obs rows from registers only for small launches of multi-team waves / block teams
+    assert info.staged_obs == (1 if lanes == 64 or info.blocks > 2048 else 0)
+
+
+def test_obs_direct_threshold(nat, lib):
+    info = nat.SwarmLaunchInfo()
+    for n, e, staged in [(16, 1024, 0), (16, 8192, 0), (16, 8193, 1), (16, 32768, 1), (256, 1024, 0),
+                         (256, 4096, 1), (64, 1024, 1), (3, 4, 0)]:
+        p = _params(nat, lib, num_drones=n, num_envs=e)
+        assert lib.swarm_query_launch(ctypes.byref(p), ctypes.byref(info)) == 0
+        assert info.staged_obs == staged, (n, e)
 
 
 @pytest.mark.parametrize("field,value,code", [
