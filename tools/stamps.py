@@ -33,7 +33,8 @@ from swarm_marl_amd import _native as nat
 
 e = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 64
-vec = VecSwarm(e, {"num_drones": n}, device="cuda:0", auto_reset=True, seed=0)
+dyn = os.environ.get("SWARM_STAMPS_DYNAMICS", "kinematic")
+vec = VecSwarm(e, {"num_drones": n}, device="cuda:0", auto_reset=True, seed=0, dynamics=dyn)
 vec.reset()
 lib = nat.load_library()
 lib.swarm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
