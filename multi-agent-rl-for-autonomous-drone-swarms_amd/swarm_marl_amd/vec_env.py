@@ -36,6 +36,11 @@ PHYSICS_DEFAULTS = dict(gravity=-9.81, gravity_comp=9.5, substep_dt=1.0 / 240.0,
                         drone_contact_radius=0.15, ground_contact_height=0.025, damping_law=0)
 
 
+# torch's raw current-stream handle (what torch.cuda.current_stream(d).cuda_stream returns,
+# without constructing a Stream object); the public call is the fallback
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _ptr(t: torch.Tensor | None) -> int | None:
     return None if t is None else t.data_ptr()
 
@@ -127,6 +132,12 @@ class VecSwarm:
             self.group_launch_info.append(li)
         self.group_streams = ([torch.cuda.Stream(self.device) for _ in range(g_n)]
                               if g_n > 1 else None)
+        self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self._swarm_step = self.lib.swarm_step
+        self._gstream_h = [st.cuda_stream for st in self.group_streams] if self.group_streams else []
+        # fork / join events of the group launches, reused by every step (record overwrites)
+        self._fork_ev = torch.cuda.Event() if g_n > 1 else None
+        self._join_evs = [torch.cuda.Event() for _ in range(g_n)] if g_n > 1 else []
 
         e, m, d = self.num_envs, int(cfg.num_obstacles), self.obs_dim
         kw = dict(device=self.device)
@@ -226,18 +237,26 @@ class VecSwarm:
             self._gstate.append(s)
             self._gout.append(o)
         self._state_c, self._out_c = self._gstate[0], self._gout[0]
+        # per-launch plumbing built once (eager steps are host-bound at small E or with groups):
+        # the three struct references and each group's row offsets into an [E,N,3] f32 actions
+        # tensor / [E,N] u8 action mask (both validated contiguous by _actions)
+        self._grefs = [(ctypes.byref(self._gparams[g]), ctypes.byref(self._gstate[g]), ctypes.byref(self._gout[g]))
+                       for g in range(self.groups)]
+        self._gact_off = [(lo * self.num_drones * 12, lo * self.num_drones) for lo, _ in self.group_slices]
 
     def _stream(self) -> int:
+        if _RAW_STREAM is not None:  # the raw handle, no Stream object per call
+            return _RAW_STREAM(self._dev_index)
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def _check_tensor(self, name: str, t: torch.Tensor, shape: tuple, dtype) -> None:
         if not isinstance(t, torch.Tensor):
             raise ValueError(f"{name} must be a torch.Tensor")
-        if t.device != self.device:
+        if not t.is_cuda or t.get_device() != self._dev_index:
             raise ValueError(f"{name} is on {t.device}, expected {self.device}")
         if t.dtype != dtype:
             raise ValueError(f"{name} has dtype {t.dtype}, expected {dtype}")
-        if tuple(t.shape) != tuple(shape):
+        if t.shape != shape:
             raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
         if not t.is_contiguous():
             raise ValueError(f"{name} must be contiguous")
@@ -263,12 +282,12 @@ class VecSwarm:
         return actions, action_mask
 
     def _launch_step(self, g: int, actions, action_mask, stream: int) -> None:
-        lo = self.group_slices[g][0]
-        a = actions.data_ptr() + lo * actions.stride(0) * actions.element_size()
-        am = None if action_mask is None else action_mask.data_ptr() + lo * action_mask.stride(0)
-        rc = self.lib.swarm_step(ctypes.byref(self._gparams[g]), ctypes.byref(self._gstate[g]), a, am,
-                                 ctypes.byref(self._gout[g]), stream)
-        nat.check(rc, self.lib)
+        pr, sr, orf = self._grefs[g]
+        ao, mo = self._gact_off[g]
+        rc = self._swarm_step(pr, sr, actions.data_ptr() + ao,
+                              None if action_mask is None else action_mask.data_ptr() + mo, orf, stream)
+        if rc:
+            nat.check(rc, self.lib)
 
     def step(self, actions: torch.Tensor, action_mask: torch.Tensor | None = None, *,
              join: bool = True):
@@ -286,11 +305,11 @@ class VecSwarm:
             self._launch_step(0, actions, action_mask, self._stream())
             return self.obs, self.reward, self.terminated, self.truncated, self.env_done
         cur = torch.cuda.current_stream(self.device)
-        fork = torch.cuda.Event()
+        fork = self._fork_ev
         fork.record(cur)
         for g, st in enumerate(self.group_streams):
             st.wait_event(fork)
-            self._launch_step(g, actions, action_mask, st.cuda_stream)
+            self._launch_step(g, actions, action_mask, self._gstream_h[g])
             if not join:  # the caller's tensors are in use on the group stream
                 actions.record_stream(st)
                 if action_mask is not None:
@@ -314,8 +333,9 @@ class VecSwarm:
         if self.group_streams is None:
             return
         cur = torch.cuda.current_stream(self.device)
-        for st in self.group_streams:
-            cur.wait_stream(st)
+        for st, ev in zip(self.group_streams, self._join_evs):
+            ev.record(st)
+            cur.wait_event(ev)
 
     def _aux(self, fn, env_mask) -> None:
         self.join()
