@@ -42,7 +42,7 @@ class DronePhysicsEnv(MultiAgentEnv):
         self.masses = np.ones(self.num_drones, np.float32)
         self._vec = VecSwarm(1, self.cfg, num_drones=self.num_drones, dynamics="physics",
                              auto_reset=False, with_infos=True, with_global_state=True,
-                             physics=physics, packed_io=True)
+                             physics=physics, packed_io="mapped")
         self._io = PackedIO(self._vec)
 
     @property

@@ -49,7 +49,7 @@ class DroneSwarmEnv(MultiAgentEnv):
         self.action_space = Box(low=-1.0, high=1.0, shape=(3,), dtype=np.float32)
         self._vec = VecSwarm(1, self.cfg, num_drones=self.num_drones, dynamics="kinematic",
                              auto_reset=False, with_infos=True, with_global_state=True,
-                             packed_io=True)
+                             packed_io="mapped")
         self._vec.active.fill_(True)
         self._io = PackedIO(self._vec)
 
@@ -141,16 +141,22 @@ class PackedIO:
 
     def __init__(self, vec: VecSwarm):
         self.vec = vec
-        self._hin = torch.empty(vec.in_arena.shape, dtype=torch.uint8, pin_memory=True)
-        self._hout = torch.empty(vec.out_arena.shape, dtype=torch.uint8, pin_memory=True)
+        self.mapped = vec.mapped_io
+        if self.mapped:  # the arenas are pinned host memory the kernel uses in place: no mirrors
+            self._hin, self._hout = vec.in_arena, vec.out_arena
+        else:
+            self._hin = torch.empty(vec.in_arena.shape, dtype=torch.uint8, pin_memory=True)
+            self._hout = torch.empty(vec.out_arena.shape, dtype=torch.uint8, pin_memory=True)
         self.h_in = {k: t.numpy() for k, t in VecSwarm.arena_views(self._hin, vec.in_layout).items()}
         self.h_out = {k: t.numpy() for k, t in VecSwarm.arena_views(self._hout, vec.out_layout).items()}
 
     def send(self) -> None:
-        self.vec.in_arena.copy_(self._hin, non_blocking=True)
+        if not self.mapped:
+            self.vec.in_arena.copy_(self._hin, non_blocking=True)
 
     def fetch(self) -> dict[str, np.ndarray]:
-        self._hout.copy_(self.vec.out_arena, non_blocking=True)
+        if not self.mapped:
+            self._hout.copy_(self.vec.out_arena, non_blocking=True)
         torch.cuda.current_stream(self.vec.device).synchronize()
         return self.h_out
 

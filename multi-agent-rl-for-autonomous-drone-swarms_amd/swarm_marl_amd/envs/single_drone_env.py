@@ -34,7 +34,7 @@ class SingleDroneEnv(GymEnv):
         self.step_count = 0
         self._vec = VecSwarm(1, replace(self.cfg, neighbor_k=0, max_steps=2 ** 31 - 1),
                              num_drones=1, dynamics="kinematic", auto_reset=False,
-                             with_infos=True, packed_io=True)
+                             with_infos=True, packed_io="mapped")
         self._io = PackedIO(self._vec)
 
     @property

@@ -41,6 +41,29 @@ PHYSICS_DEFAULTS = dict(gravity=-9.81, gravity_comp=9.5, substep_dt=1.0 / 240.0,
 _RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
+# mapped packed I/O is for dict-API sized batches (one env of a few drones): the kernel's reads
+# and writes then cross the host link, which only pays when the copies' fixed costs dominate
+MAPPED_IO_MAX_AGENTS = 1024
+_HIP = None
+
+
+def _device_mapped(host_ptr: int) -> bool:
+    """True when the HIP runtime maps this pinned host allocation into the device address space
+    at the same address (hipHostGetDevicePointer), i.e. a kernel may dereference host_ptr."""
+    global _HIP
+    try:
+        if _HIP is None:
+            _HIP = ctypes.CDLL("libamdhip64.so")
+            _HIP.hipHostGetDevicePointer.restype = ctypes.c_int
+            _HIP.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p,
+                                                     ctypes.c_uint]
+        d = ctypes.c_void_p()
+        rc = _HIP.hipHostGetDevicePointer(ctypes.byref(d), ctypes.c_void_p(host_ptr), 0)
+        return rc == 0 and d.value == host_ptr
+    except (OSError, AttributeError):
+        return False
+
+
 def _ptr(t: torch.Tensor | None) -> int | None:
     return None if t is None else t.data_ptr()
 
@@ -150,13 +173,21 @@ class VecSwarm:
         # packed_io (the dict-API envs): the per-step inputs (an actions buffer and the active
         # mask) and all outputs are views of two flat device arenas, so that one step moves one
         # H2D and one D2H copy (in_layout / out_layout: name -> (byte offset, shape, dtype))
+        if packed_io not in (False, True, "mapped"):
+            raise ValueError(f"packed_io must be False, True or 'mapped', got {packed_io!r}")
         self.packed_io = bool(packed_io)
+        # "mapped": the arenas are pinned host memory the kernel reads and writes in place (the
+        # device address of a pinned allocation is its host address), so a dict-API step moves
+        # no copies at all: the host fills the inputs, launches, synchronises and reads the
+        # outputs.  Used only when the runtime confirms the mapping; otherwise device arenas.
+        self.mapped_io = packed_io == "mapped" and self.num_envs * n <= MAPPED_IO_MAX_AGENTS
         self.in_arena = self.out_arena = None
         self.in_layout, self.out_layout = {}, {}
         if self.packed_io:
             self.in_arena, views = self._arena(self.in_layout, [
                 ("actions", (e, n, 3), f32), ("active", (e, n), torch.bool),
-                ("action_mask", (e, n), torch.uint8)], self.device)
+                ("action_mask", (e, n), torch.uint8)], self.device, self.mapped_io)
+            self.mapped_io = self.in_arena.device.type == "cpu"
             self.actions_in = views["actions"]
             self.action_mask_in = views["action_mask"]
             self.active = views["active"]
@@ -184,7 +215,8 @@ class VecSwarm:
         if with_infos:
             outs.append(("info_flags", (e, n), torch.uint8))
         if self.packed_io:
-            self.out_arena, views = self._arena(self.out_layout, outs, self.device)
+            self.out_arena, views = self._arena(self.out_layout, outs, self.device, self.mapped_io)
+            self.mapped_io = self.mapped_io and self.out_arena.device.type == "cpu"
         else:
             views = {name: torch.zeros(shape, dtype=dt, **kw) for name, shape, dt in outs}
         for name in ("obs", "reward", "terminated", "truncated", "env_done", "dist_goal",
@@ -194,15 +226,22 @@ class VecSwarm:
 
     # ------------------------------------------------------------------ plumbing
     @staticmethod
-    def _arena(layout: dict, fields, device):
+    def _arena(layout: dict, fields, device, mapped: bool = False):
         """One zeroed uint8 buffer holding `fields` (name, shape, dtype) at 16-B aligned offsets;
-        returns (buffer, {name: typed view}) and fills `layout`."""
+        returns (buffer, {name: typed view}) and fills `layout`.  mapped: pinned host memory
+        whose device address equals its host address (else a device buffer)."""
         off = 0
         for name, shape, dt in fields:
             nbytes = torch.Size(shape).numel() * torch.empty((), dtype=dt).element_size()
             layout[name] = (off, tuple(shape), dt)
             off += (nbytes + 15) // 16 * 16
-        buf = torch.zeros((max(off, 16),), dtype=torch.uint8, device=device)
+        buf = None
+        if mapped:
+            buf = torch.zeros((max(off, 16),), dtype=torch.uint8).pin_memory()
+            if not _device_mapped(buf.data_ptr()):
+                buf = None
+        if buf is None:
+            buf = torch.zeros((max(off, 16),), dtype=torch.uint8, device=device)
         return buf, VecSwarm.arena_views(buf, layout)
 
     @staticmethod
@@ -273,6 +312,9 @@ class VecSwarm:
 
     # ------------------------------------------------------------------ API
     def _actions(self, actions, action_mask):
+        if self.mapped_io and actions is self.actions_in and (action_mask is None or
+                                                              action_mask is self.action_mask_in):
+            return actions, action_mask  # the mapped arena's own views (host-resident, device-addressable)
         self._check_tensor("actions", actions, (self.num_envs, self.num_drones, 3), torch.float32)
         if action_mask is not None:
             if action_mask.dtype == torch.bool:
@@ -359,6 +401,8 @@ class VecSwarm:
                   step_count=None, episode=None, damping=None) -> None:
         """Inject state (host or device arrays); shapes as the state tensors."""
         self.join()
+        if self.mapped_io:  # `active` lives in the mapped arena: no kernel may still use it
+            torch.cuda.current_stream(self.device).synchronize()
         for name, val in (("pos", pos), ("vel", vel), ("goal", goal), ("obstacles", obstacles),
                           ("active", active), ("step_count", step_count),
                           ("episode", episode), ("damping", damping)):
