@@ -16,8 +16,10 @@ rate without per-step host launch cost); HIP events recorded on the launch strea
 timed region give the average launch duration (`roofline.kernel_ms_mean`, the roofline's time
 base; compare `rocprofv3 --kernel-trace --stats` in profiles/).  A second, eager pass with one
 event pair per launch is reported as `ms_per_step_eager` / `kernel_ms_eager_events`.
-`--ctde` also emits the CTDE global_state and all-gathers it every `--gather-every` steps over
-RCCL (config 5; eager timing).
+`--ctde` also emits the CTDE global_state and, with several ranks, all-gathers it every
+`--gather-every` steps over RCCL on a side stream, overlapped with the following steps (a
+`--gs-slots` device ring; swarm_marl_amd.distributed.GlobalStateGather; config 5; eager timing).
+Under SWARM_BENCH_REHEARSAL (gloo, every rank on cuda:0) the gather is staged through host memory.
 
 `cpu_baseline` = the C port of the reference step (oracle/swarm_oracle.c) on the host cores for
 a bounded sample of the same workload; `cpu_baseline_variants` = the per-agent loop restatement
@@ -94,10 +96,12 @@ def parse(argv=None):
                          "warm-up steps (GPU clocks ramp over ~100 ms; reported in the JSON line)")
     ap.add_argument("--groups", type=int, default=None,
                     help="env groups per GPU, each stepped on its own HIP stream (VecSwarm groups=G); "
-                         "default 2 for the headline and n256 (1 for n256 with a multi-rank CTDE "
-                         "gather), 1 for n16")
+                         "default 2 for the headline and n256, 1 for n16")
     ap.add_argument("--gather-every", type=int, default=8,
                     help="CTDE all-gather period in steps (SURVEY.md §5: per batch, not per step)")
+    ap.add_argument("--gs-slots", type=int, default=4,
+                    help="CTDE global_state ring slots (multi-rank): a gathered slot is rewritten "
+                         "only R steps later, so the gather overlaps R-1 steps")
     a = ap.parse_args(argv)
     pre = PRESETS[a.config]
     a.drones = pre["drones"] if a.drones is None else a.drones
@@ -112,6 +116,8 @@ def parse(argv=None):
 
     if a.gather_every < 1:
         ap.error("--gather-every must be >= 1")
+    if a.gs_slots < 1:
+        ap.error("--gs-slots must be >= 1")
     return a
 
 
@@ -254,8 +260,6 @@ def main(argv=None):
     # SWARM_BENCH_REHEARSAL=1: every rank on cuda:0 with the gloo backend — the multi-rank code
     # path (sharding, barriers, max-reduce) rehearsed on a one-GPU box; not a scaling measurement
     rehearsal = os.environ.get("SWARM_BENCH_REHEARSAL") == "1"
-    if rehearsal and args.ctde:
-        raise SystemExit("SWARM_BENCH_REHEARSAL runs without --ctde (the gather needs RCCL)")
     if world > 1:
         if not rehearsal:
             torch.cuda.set_device(local)
@@ -267,16 +271,17 @@ def main(argv=None):
 
     n = args.drones
     offset, e = shard_plan(world, rank, args.envs)
-    if args.ctde and world > 1 and args.groups > 1:  # the gather reads the whole batch each period
-        if args.groups_explicit:
-            raise SystemExit("--ctde with several ranks gathers the whole batch's global_state: use --groups 1")
-        args.groups = 1
+    # SWARM_BENCH_FORCE_GATHER=1: run the gather with a one-rank process group the caller set
+    # up (tests/test_gpu_ctde.py drives this branch over RCCL on one GPU)
+    gathering = args.ctde and (world > 1 or (os.environ.get("SWARM_BENCH_FORCE_GATHER") == "1"
+                                             and dist.is_initialized()))
     raw = {"num_drones": n}
     if args.no_term:
         raw.update(collision_radius=0.0, obstacle_radius=0.0, goal_radius=0.0)
     vec = VecSwarm(e, raw, device=dev, auto_reset=True, seed=0, env_offset=offset, dynamics=args.dynamics,
                    with_global_state=args.ctde, persistent=not args.no_persistent,
-                   waves_per_simd=args.waves_per_simd, groups=args.groups)
+                   waves_per_simd=args.waves_per_simd, groups=args.groups,
+                   global_state_slots=args.gs_slots if gathering else 1)
     vec.reset()
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     ring = [torch.rand((e, n, 3), device=dev, generator=gen) * 2 - 1 for _ in range(args.ring)]
@@ -290,10 +295,14 @@ def main(argv=None):
                                     rng.normal(0, 0.01, (6, 256)), np.zeros(6), device=dev,
                                     precision=args.policy)
         pol_act = torch.zeros((e, n, 3), device=dev)
-    gather_buf = None
+    gatherer = None
     gathers = set()
-    if args.ctde and world > 1:
-        gather_buf = torch.empty((world * e, 6 * n + 3), device=dev)
+    if gathering:
+        # CTDE: every step writes global_state into slot k % R of a device ring; the gather
+        # steps' slots are all-gathered on a side stream while the next steps run (RCCL; the
+        # gloo rehearsal stages through pinned host memory), distributed.GlobalStateGather
+        from swarm_marl_amd.distributed import GlobalStateGather
+        gatherer = GlobalStateGather(vec.global_state_ring, vec.select_global_state_slot)
         gathers = set(gather_schedule(args.steps, args.gather_every))
 
     G = vec.groups
@@ -315,14 +324,19 @@ def main(argv=None):
             with torch.cuda.stream(st):
                 env_step_group(g, k)
 
+    launch_streams = vec.group_streams if G > 1 else [torch.cuda.current_stream(dev)]
+
     def step(k):
+        if gatherer is None:
+            env_step(k)
+            return
+        gatherer.before_step(launch_streams)
         env_step(k)
-        if gather_buf is not None and k in gathers:
-            vec.join()
-            dist.all_gather_into_tensor(gather_buf, vec.global_state)
+        gatherer.after_step(launch_streams, gather=k in gathers)
 
     stream = torch.cuda.current_stream(dev)
     sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+    sync()  # the reset and the action ring are done before any group stream steps
     for k in range(args.warmup):
         step(k)
     sync()
@@ -342,13 +356,15 @@ def main(argv=None):
         if G > 1:
             for st in vec.group_streams[1:]:
                 stream.wait_stream(st)
+        if gatherer is not None:  # the timed region ends after the last gather
+            stream.wait_stream(gatherer.stream)
 
     # ---- timed region: hipGraph replay of ring segments (or eager with --no-graph / CTDE)
     # With env groups: one graph per group, captured and replayed on its group stream; the
     # events on the launch stream fork to / join from the group streams, so they bracket the
     # whole batch's K steps.
     t_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-    use_graph = not args.no_graph and gather_buf is None
+    use_graph = not args.no_graph and gatherer is None
     reps, rem = divmod(args.steps, args.ring)
     if use_graph:
         def capture(n_steps):  # one graph of n_steps ring steps per group, on its group stream
@@ -409,14 +425,16 @@ def main(argv=None):
             join()
             t_ev[1].record(stream)
         timing = "eager launches" + (f", {G} env groups on {G} HIP streams" if G > 1 else "") + (
-            f", CTDE all-gather every {args.gather_every} steps" if gather_buf is not None else "")
+            f", CTDE all-gather every {args.gather_every} steps on a side stream ({args.gs_slots}-slot "
+            f"global_state ring{', gloo host-staged' if gatherer is not None and gatherer.staged else ''})"
+            if gatherer is not None else "")
     # device warm-up: untimed ring segments until the clocks have ramped (not part of W or K)
     warm_ms, warm_steps = 0.0, 0
     if args.device_warmup_ms > 0:
         sync()
         t0 = time.perf_counter()
         # time-based unless a step holds a collective (every rank must then run the same count)
-        fixed = None if gather_buf is None else max(args.ring, int(args.device_warmup_ms * 5))
+        fixed = None if gatherer is None else max(args.ring, int(args.device_warmup_ms * 5))
         while ((time.perf_counter() - t0) * 1e3 < args.device_warmup_ms if fixed is None
                else warm_steps < fixed):
             if use_graph:
@@ -430,6 +448,7 @@ def main(argv=None):
                 sync()
         sync()
         warm_ms = (time.perf_counter() - t0) * 1e3
+    gather_t0 = gatherer.k if gatherer is not None else 0
     wall = timed_region(body, world, sync)
     kern_ms = t_ev[0].elapsed_time(t_ev[1]) / args.steps
 
@@ -529,8 +548,11 @@ def main(argv=None):
                        "obs_dim": vec.obs_dim,
                        "parallelism": f"env-sharded x{world}" + (f", {G} env groups per GPU on {G} HIP streams"
                                                                   if G > 1 else ""),
-                       "ctde_allgather": bool(gather_buf is not None),
-                       "ctde_gather_every": args.gather_every if gather_buf is not None else None},
+                       "ctde_allgather": gatherer is not None,
+                       "ctde_gather_every": args.gather_every if gatherer is not None else None,
+                       "ctde_gathers_timed": (sum(1 for k in gatherer.gathered_steps if k >= gather_t0)
+                                              if gatherer is not None else None),
+                       "ctde_gather_backend": gatherer.backend if gatherer is not None else None},
             "roofline": roof,
             "env_done_fraction_last_step": done_frac,
             **({"rehearsal": f"{world} ranks sharing cuda:0 over gloo (SWARM_BENCH_REHEARSAL): the "

@@ -61,6 +61,8 @@
 #define ABL_STORE_ONLY 128  // step64: obs stores straight from registers (wrong values)
 #define ABL_STAGE_ONLY 256  // step64: obs staged through LDS, not stored
 #define ABL_ROW_ONLY 512    // step64: obs row computed, neither staged nor stored
+#define ABL_RESET_WORK 1024 // step64: a resetting env draws its new state but skips its key passes,
+                            // finish and obs (wrong obs; the dynamics are unchanged)
 
 // Diagnostic phase timestamps (tools/stamps.py; never set in the product build)
 #ifdef SWARM_STAMPS
@@ -1829,16 +1831,18 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     gz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(goal_z), M));
     s64_put(ring, soa, t, px, py, pz, 1.f);
     wave_sync();
+    if (!(SWARM_ABLATE & ABL_RESET_WORK)) {
 #pragma unroll
-    for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
+      for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
 #pragma unroll
-    for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
-    bool c2 = false;
-    float s2 = 0.f;
-    double f2 = 0.0;
-    pair_pass_s64<KS, 0, true>(soa, t, px, py, pz, true, A->P.nb_keep, 0.f, nk, s2, f2);
-    obstacle_pass_s64<MSL, false>(osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
-    select_topk(false);
+      for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
+      bool c2 = false;
+      float s2 = 0.f;
+      double f2 = 0.0;
+      pair_pass_s64<KS, 0, true>(soa, t, px, py, pz, true, A->P.nb_keep, 0.f, nk, s2, f2);
+      obstacle_pass_s64<MSL, false>(osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
+      select_topk(false);
+    }
   } else {
     select_topk(DYN == DYN_KIN);  // the kinematic step pass ranks by d~, physics by s'
   }

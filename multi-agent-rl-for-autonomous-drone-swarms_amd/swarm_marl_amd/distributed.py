@@ -22,6 +22,115 @@ def shard_bounds(num_envs_global: int, world_size: int, rank: int) -> tuple[int,
     return offset, count
 
 
+class GlobalStateGather:
+    """Periodic CTDE global_state all-gather, overlapped with the steps that follow it.
+
+    The reference builds the critic input per step (drone_swarm_env.py:293-302, collected into
+    the batch by training/callbacks.py:14-57; global_state_dim = 6N+3, config_builders.py:164).
+    Here each step writes the state into slot k % R of a device ring `ring` [R, E_local, 6N+3]
+    (`select_slot(i)` points the next launch at slot i: VecSwarm.select_global_state_slot).  A
+    gather step's slot is all-gathered on a side stream once that step's launches are done,
+    while the next steps run on their own streams; only the step that next rewrites the slot
+    (R steps later) waits for the gather.  With R = 1 and no side stream this degenerates to
+    the synchronous join-then-gather.
+
+    Backends: "nccl" (RCCL over xGMI) gathers device tensors directly.  "gloo" (the CPU test
+    backend and bench.py's one-GPU rehearsal) gathers host tensors: a device ring is staged
+    through pinned host memory on the side stream (synchronously, so no overlap there).
+    A CPU ring (tests) is gathered in place.
+
+    Usage per step k:  g.before_step(streams); <launch step k on streams>; g.after_step(streams, k in sched)
+    then g.wait() before reading `g.result(i)` of the i-th gather on the current stream.
+    """
+
+    def __init__(self, ring: torch.Tensor, select_slot, *, group=None, keep: int = 2):
+        if ring.dim() != 3:
+            raise ValueError("ring must be [slots, E_local, F]")
+        self.ring, self.select_slot, self.group = ring, select_slot, group
+        self.slots = int(ring.shape[0])
+        self.dist = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.dist else 1
+        self.backend = dist.get_backend(group) if self.dist else None
+        self.cuda = ring.is_cuda
+        self.staged = self.cuda and self.backend == "gloo"
+        e, f = int(ring.shape[1]), int(ring.shape[2])
+        # `keep` result buffers, used round robin: gather i lands in outs[i % keep]
+        self.outs = [torch.empty((self.world * e, f), dtype=ring.dtype, device=ring.device)
+                     for _ in range(max(1, keep))]
+        self.k = 0        # steps seen
+        self.count = 0    # gathers issued
+        self.gathered_steps: list[int] = []
+        if self.cuda:
+            self.stream = torch.cuda.Stream(ring.device)
+            self.slot_done = [torch.cuda.Event() for _ in range(self.slots)]
+            self.slot_pending = [False] * self.slots
+            self._step_evs: list = []
+            if self.staged:
+                self.h_in = torch.empty((e, f), dtype=ring.dtype).pin_memory()
+                self.h_out = torch.empty((self.world * e, f), dtype=ring.dtype)
+
+    def before_step(self, streams=()) -> int:
+        """Point the next step at its slot; the streams that will rewrite a slot still being
+        gathered wait for that gather first.  Returns the slot."""
+        s = self.k % self.slots
+        if self.cuda and self.slot_pending[s]:
+            for st in streams:
+                st.wait_event(self.slot_done[s])
+            self.slot_pending[s] = False
+        self.select_slot(s)
+        return s
+
+    def after_step(self, streams=(), gather: bool = False) -> None:
+        """Called after step k's launches were issued on `streams`; gathers its slot if asked."""
+        s = self.k % self.slots
+        step = self.k
+        self.k += 1
+        if not gather:
+            return
+        out = self.outs[self.count % len(self.outs)]
+        self.count += 1
+        self.gathered_steps.append(step)
+        src = self.ring[s]
+        if not self.cuda:
+            self._gather(out, src)
+            return
+        while len(self._step_evs) < len(streams):
+            self._step_evs.append(torch.cuda.Event())
+        for st, ev in zip(streams, self._step_evs):
+            ev.record(st)
+            self.stream.wait_event(ev)
+        with torch.cuda.stream(self.stream):
+            if self.staged:  # gloo: host tensors only
+                self.h_in.copy_(src, non_blocking=True)
+                self.stream.synchronize()
+                self._gather(self.h_out, self.h_in)
+                out.copy_(self.h_out, non_blocking=True)
+            else:
+                self._gather(out, src)
+            self.slot_done[s].record(self.stream)
+        self.slot_pending[s] = True
+
+    def _gather(self, out: torch.Tensor, src: torch.Tensor) -> None:
+        if self.dist:  # the collective even for one rank (the -m gpu test drives RCCL this way)
+            dist.all_gather_into_tensor(out, src, group=self.group)
+        else:
+            out.copy_(src, non_blocking=True)
+
+    def wait(self) -> None:
+        """Make the current stream wait for every gather issued so far."""
+        if self.cuda:
+            torch.cuda.current_stream(self.ring.device).wait_stream(self.stream)
+
+    def result(self, i: int = -1) -> torch.Tensor:
+        """Buffer of gather i (default: the latest); valid until `keep` further gathers."""
+        if self.count == 0:
+            raise RuntimeError("no gather issued yet")
+        i = self.count - 1 if i < 0 else i
+        if not self.count - len(self.outs) <= i < self.count:
+            raise IndexError(f"gather {i} was overwritten (keep={len(self.outs)})")
+        return self.outs[i % len(self.outs)]
+
+
 def gather_global_state(local: torch.Tensor, group=None) -> torch.Tensor:
     """All-gather the per-env CTDE critic input [E_local, 6N+3] into [E_global, 6N+3].
 

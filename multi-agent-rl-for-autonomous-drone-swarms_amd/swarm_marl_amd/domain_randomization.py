@@ -106,13 +106,30 @@ class DomainRandomizer:
     def sample(self) -> dict[str, torch.Tensor]:
         return sample_values(self.base, self.ranges, self.vec.num_envs, self.generator, self.vec.device)
 
-    def begin(self) -> None:
-        """Draw the current episode's parameters of every env (call before vec.reset()) and the
-        next episode's."""
+    def begin(self, reset: bool = True):
+        """Start every env on its own draw and queue a different draw for its next episode.
+
+        A device reset copies `env_cfg_next` into the current record (swarm_kernel.hip draw_env),
+        so the first episode's draw goes into `next`, the reset switches it in, and a fresh draw
+        then refills `next` — otherwise the first two episodes of every env would share one draw.
+        reset=True performs that vec.reset() here and returns its obs; with reset=False the
+        caller must reset and then call `after_reset()`."""
+        if not self.enabled or not self.ranges:
+            return self.vec.reset() if reset else None
+        self.vec.set_env_config(**self.sample())  # current records exist before the first reset
+        self.vec.set_env_config(next_episode=True, **self.sample())
+        if not reset:
+            return None
+        obs = self.vec.reset()
+        self.after_reset()
+        return obs
+
+    def after_reset(self, env_mask: torch.Tensor | None = None) -> None:
+        """Fresh next-episode draws for the envs an explicit vec.reset(env_mask) just started
+        (all if None): the reset consumed their queued draw."""
         if not self.enabled or not self.ranges:
             return
-        self.vec.set_env_config(**self.sample())
-        self.vec.set_env_config(next_episode=True, **self.sample())
+        self.vec.set_env_config(next_episode=True, env_mask=env_mask, **self.sample())
 
     def after_step(self) -> None:
         """Fresh next-episode draws for the envs the last step reset (they started the drawn

@@ -71,9 +71,12 @@ class EvalTracker:
         self.last = torch.zeros_like(self.start)
         self.traveled = torch.zeros((e, n), **f64)
         seg = nat.EVAL_SEGMENTS
-        # segment s holds the episodes of global envs g with g % 64 == s: capacity per segment
-        # sized for the busiest one (ceil(E / 64) envs, `capacity` episodes per env on average)
-        self.capacity = max(seg, -(-int(capacity) // seg) * seg)
+        # segment s holds the episodes of global envs g with g % 64 == s, so only min(E, 64)
+        # segments are ever written and the busiest holds ceil(E / 64) envs: size every segment
+        # for that one's share of `capacity` episodes (capacity * ceil(E/64) / E), so that
+        # `capacity` finished episodes fit whatever E is (E = 8: 8 live segments, not 64)
+        seg_cap = max(1, -(-int(capacity) * (-(-e // seg)) // e))
+        self.capacity = seg * seg_cap
         self.records_buf = torch.zeros((self.capacity, nat.EVAL_RECORD), **f64)
         self.count = torch.zeros(seg, dtype=torch.int32, device=dev)
         self.updates = 0
@@ -124,6 +127,11 @@ class EvalTracker:
         c.state_pos = v.pos.data_ptr() + lo * v.pos.stride(0) * v.pos.element_size()
         c.state_goal = v.goal.data_ptr() + lo * v.goal.stride(0) * v.goal.element_size()
         return c
+
+    def overflowed(self) -> bool:
+        """True once a record segment has filled (further episodes of its envs are dropped by
+        the kernel): one 256-B device read, for long runs to check every few thousand updates."""
+        return int(self.count.max()) > self.capacity // nat.EVAL_SEGMENTS
 
     def records(self) -> np.ndarray:
         """Finished-episode records [n, 9] (FIELDS), in completion order: by the update that

@@ -75,7 +75,7 @@ class VecSwarm:
                  device: str | torch.device | None = None, with_infos: bool = False,
                  with_global_state: bool = False, physics: dict[str, Any] | None = None,
                  kernel_path: str = "auto", persistent: bool = True, waves_per_simd: int = 0,
-                 groups: int = 1, packed_io: bool = False):
+                 groups: int = 1, packed_io: bool = False, global_state_slots: int = 1):
         if isinstance(config, DroneEnvConfig):
             cfg, raw = config, {}
         else:
@@ -208,7 +208,18 @@ class VecSwarm:
         outs = [("obs", (e, n, d), f32), ("reward", (e, n), f32)]
         if with_infos:
             outs.append(("dist_goal", (e, n), f32))
-        if with_global_state:
+        # global_state ring (CTDE gather overlap, distributed.GlobalStateGather): the step writes
+        # slot `global_state_slot` of global_state_ring [R, E, 6N+3]; `global_state` is that slot
+        self.global_state_ring = None
+        self.global_state_slot = 0
+        gs_slots = int(global_state_slots)
+        if gs_slots < 1:
+            raise ValueError(f"global_state_slots must be >= 1, got {global_state_slots}")
+        if with_global_state and gs_slots > 1:
+            if packed_io:
+                raise ValueError("global_state_slots > 1 is not supported with packed_io")
+            self.global_state_ring = torch.zeros((gs_slots, e, 6 * n + 3), dtype=f32, **kw)
+        elif with_global_state:
             outs.append(("global_state", (e, 6 * n + 3), f32))
         outs += [("terminated", (e, n), torch.bool), ("truncated", (e, n), torch.bool),
                  ("env_done", (e,), torch.uint8)]
@@ -222,7 +233,25 @@ class VecSwarm:
         for name in ("obs", "reward", "terminated", "truncated", "env_done", "dist_goal",
                      "info_flags", "global_state"):
             setattr(self, name, views.get(name))
+        if self.global_state_ring is not None:
+            self.global_state = self.global_state_ring[0]
         self._bind()
+
+    def close(self) -> None:
+        """Wait for every launch that may still use this batch's buffers.  Needed for mapped
+        arenas: they are blocks of torch's pinned-host caching allocator that the kernels use
+        behind torch's back (no stream use is recorded on them), so dropping the VecSwarm while a
+        step is in flight could hand a block that a kernel still writes to another pinned copy.
+        Called by __del__ for mapped batches; device-resident batches need nothing."""
+        if not getattr(self, "mapped_io", False):
+            return
+        try:
+            torch.cuda.synchronize(self.device)
+        except Exception:  # interpreter shutdown: the runtime may already be gone
+            pass
+
+    def __del__(self):
+        self.close()
 
     # ------------------------------------------------------------------ plumbing
     @staticmethod
@@ -282,6 +311,23 @@ class VecSwarm:
         self._grefs = [(ctypes.byref(self._gparams[g]), ctypes.byref(self._gstate[g]), ctypes.byref(self._gout[g]))
                        for g in range(self.groups)]
         self._gact_off = [(lo * self.num_drones * 12, lo * self.num_drones) for lo, _ in self.group_slices]
+
+    def select_global_state_slot(self, i: int) -> None:
+        """Make the next launches write global_state into slot i of `global_state_ring` (and
+        `global_state` that slot).  Launches already issued keep the slot they were given."""
+        if self.global_state_ring is None:
+            if i != 0:
+                raise ValueError("this VecSwarm has one global_state buffer (global_state_slots=1)")
+            return
+        r = self.global_state_ring
+        if not 0 <= i < r.shape[0]:
+            raise ValueError(f"global_state slot {i} out of range [0, {r.shape[0]})")
+        self.global_state_slot = int(i)
+        self.global_state = r[i]
+        base = self.global_state.data_ptr()
+        row = self.global_state.stride(0) * self.global_state.element_size()
+        for g, (lo, _) in enumerate(self.group_slices):
+            self._gout[g].global_state = base + lo * row
 
     def _stream(self) -> int:
         if _RAW_STREAM is not None:  # the raw handle, no Stream object per call

@@ -1,7 +1,7 @@
 """CPU, world_size 2 over gloo: bench.py's multi-rank logic with CPU stand-in steps.
 
 The same functions bench.main() uses on the GPU (shard_plan, timed_region, max_over_ranks,
-gather_schedule + the CTDE all_gather_into_tensor) drive a C-oracle stand-in for the step on
+gather_schedule + the CTDE distributed.GlobalStateGather over a global_state slot ring) drive a C-oracle stand-in for the step on
 each rank.  Checks: the weak-scaling shards equal one run over the whole batch (the reset RNG is
 keyed by the global env index), every rank sees the MAX of the per-rank timings, and the
 periodic global_state gather concatenates the shards in rank order at the scheduled steps.
@@ -40,17 +40,26 @@ def _worker(rank: int, world: int, port: int, outdir: str) -> None:
         off, cnt = bench.shard_plan(world, rank, E_PER)
         cfg = so.make_cfg(num_drones=N, max_steps=4)
         run = co.Runner(cfg, cnt, seed=9, env_offset=off, nthreads=1)
+        from swarm_marl_amd.distributed import GlobalStateGather
         sched = set(bench.gather_schedule(STEPS, EVERY))
-        buf = torch.empty((world * cnt, 6 * N + 3))
+        # bench.main's CTDE gather: a 3-slot global_state ring, slot k % 3 written by step k
+        ring = torch.full((3, cnt, 6 * N + 3), float("nan"))
+        slot = {}
+        g = GlobalStateGather(ring, lambda i: slot.__setitem__("cur", i), keep=8)
         gathered, obs = {}, []
 
         def body():
             for k in range(STEPS):
+                s = g.before_step()
+                assert s == slot["cur"] == k % 3
                 run.step(_actions(world, k)[off:off + cnt])
+                ring[s].copy_(torch.from_numpy(run.out["global_state"]))  # the kernel's write-back
                 obs.append(run.out["obs"].copy())
+                g.after_step(gather=k in sched)
                 if k in sched:
-                    dist.all_gather_into_tensor(buf, torch.from_numpy(run.out["global_state"]))
-                    gathered[k] = buf.numpy().copy()
+                    g.wait()
+                    gathered[k] = g.result().numpy().copy()
+            assert g.gathered_steps == sorted(sched)
         wall = bench.timed_region(body, world, lambda: None)
         # rank-dependent stand-in timings: every rank must get the max
         m = bench.max_over_ranks([wall, 1.0 + rank, 10.0 - rank], world)

@@ -1,0 +1,114 @@
+"""GPU: the CTDE global_state all-gather of bench.py (BASELINE config 5), overlapped.
+
+Reference contract: the critic input is the per-step global_state (drone_swarm_env.py:293-302)
+collected for every step of a batch (training/callbacks.py:14-57; global_state_dim = 6N+3,
+config_builders.py:164).  bench.py --ctde gathers it every `--gather-every` steps with
+distributed.GlobalStateGather: the step writes slot k % R of a device ring and the gather runs
+over RCCL on a side stream while the next steps run on the two env-group streams.  Here a
+one-rank RCCL process group drives that exact path and the gathered tensors must equal, bit for
+bit, a synchronous join-then-gather of a single-stream, single-buffer run of the same batch.
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture(scope="module")
+def pg():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    try:
+        yield torch.device("cuda", 0)
+    finally:
+        dist.destroy_process_group()
+
+
+def _acts(dev, e, n, k):
+    g = torch.Generator(device=dev).manual_seed(900 + k)
+    return torch.rand((e, n, 3), device=dev, generator=g) * 2 - 1
+
+
+@pytest.mark.parametrize("e,n,groups,slots,every", [(512, 64, 2, 4, 2), (96, 256, 2, 3, 1), (300, 16, 3, 2, 3)])
+def test_overlapped_gather_equals_synchronous(pg, e, n, groups, slots, every):
+    import bench
+    from swarm_marl_amd import VecSwarm
+    from swarm_marl_amd.distributed import GlobalStateGather, gather_global_state
+    dev = pg
+    steps = 11
+    sched = set(bench.gather_schedule(steps, every))
+    kw = dict(device=dev, auto_reset=True, seed=21, with_global_state=True)
+    # the bench's path: env groups on their streams, slot ring, side-stream RCCL gather, no joins
+    a = VecSwarm(e, {"num_drones": n}, groups=groups, global_state_slots=slots, **kw)
+    # reference: one launch per step on the current stream, one buffer, join + gather inline
+    b = VecSwarm(e, {"num_drones": n}, **kw)
+    a.reset()
+    b.reset()
+    g = GlobalStateGather(a.global_state_ring, a.select_global_state_slot, keep=len(sched))
+    assert g.world == 1 and g.backend == "nccl" and not g.staged
+    acts = [_acts(dev, e, n, k) for k in range(steps)]
+    for st in a.group_streams:  # the group streams start after the reset and the action draws
+        st.wait_stream(torch.cuda.current_stream(dev))
+    ref = {}
+    for k in range(steps):
+        g.before_step(a.group_streams)
+        for gi, st in enumerate(a.group_streams):
+            with torch.cuda.stream(st):
+                a.step_group(gi, acts[k])
+        g.after_step(a.group_streams, gather=k in sched)
+        b.step(acts[k])
+        if k in sched:
+            ref[k] = gather_global_state(b.global_state).clone()
+    a.join()
+    g.wait()
+    torch.cuda.synchronize()
+    assert g.gathered_steps == sorted(sched)
+    for i, k in enumerate(g.gathered_steps):
+        assert torch.equal(g.result(i), ref[k]), f"gather at step {k}"
+        # the slot that step k wrote still holds it unless a later step reused the slot
+        if k + slots >= steps:
+            assert torch.equal(a.global_state_ring[k % slots], ref[k])
+    assert torch.equal(a.obs, b.obs) and torch.equal(a.pos, b.pos)
+
+
+def test_bench_ctde_rehearsal_line_one_rank(pg, capsys):
+    """bench.main's CTDE branch end to end on one rank (RCCL group of one): the gather runs every
+    --gather-every steps inside the timed region and the line says so."""
+    import json
+    import bench
+    bench_args = ["--config", "n256", "--envs", "64", "--steps", "16", "--warmup", "2",
+                  "--device-warmup-ms", "0", "--no-cpu-baseline", "--gather-every", "4"]
+    # main() gathers only with several ranks unless SWARM_BENCH_FORCE_GATHER=1 (one-rank RCCL group)
+    import torch.distributed as dist
+    assert dist.is_initialized()
+    rec = _run_main_with_world(bench, bench_args, capsys)
+    cfg = rec["config"]
+    assert cfg["ctde_allgather"] is True and cfg["ctde_gather_every"] == 4
+    assert cfg["ctde_gathers_timed"] == 4 and cfg["ctde_gather_backend"] == "nccl"
+    assert rec["value"] > 0
+
+
+def _run_main_with_world(bench, argv, capsys):
+    old = os.environ.get("SWARM_BENCH_FORCE_GATHER")
+    os.environ["SWARM_BENCH_FORCE_GATHER"] = "1"
+    try:
+        bench.main(argv)
+    finally:
+        if old is None:
+            os.environ.pop("SWARM_BENCH_FORCE_GATHER", None)
+    line = [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][-1]
+    return json.loads(line)

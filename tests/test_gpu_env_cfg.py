@@ -202,12 +202,24 @@ def test_domain_randomizer_draws_per_episode(dev):
     vec = VecSwarm(e, {"num_drones": n, "max_steps": 4}, device=dev, auto_reset=True, seed=2)
     dr = DomainRandomizer(vec, yaml.safe_load(DR_YAML), seed=1, force=True)
     assert "dynamics.mass_scale" in dr.unsupported
-    dr.begin()
-    vec.reset()
+    dr.begin()  # resets, then queues a fresh draw for every env's next episode
+    torch.cuda.synchronize()
     cur = vec.env_config()
     ws = cur["world_size"].cpu().numpy()
     assert ws.min() >= 19.0 and ws.max() <= 21.0 and len(np.unique(ws)) == e
     assert np.allclose(cur["half_w"].cpu().numpy(), (ws / 2.0).astype(np.float32))
+    nxt = vec.env_config(True)
+    for k in ("world_size", "max_speed", "max_accel", "dt"):  # episodes 1 and 2 differ per env
+        assert bool((cur[k] != nxt[k]).all()), k
+    # an explicit reset consumes the queued draw; after_reset refills it
+    queued = {k: v.clone() for k, v in nxt.items()}
+    vec.reset()
+    dr.after_reset()
+    torch.cuda.synchronize()
+    cur, nxt = vec.env_config(), vec.env_config(True)
+    for k in ("world_size", "max_speed", "max_accel", "dt"):
+        assert torch.equal(cur[k], queued[k]), k
+        assert bool((cur[k] != nxt[k]).all()), k
     switched = 0
     for t in range(6):
         prev_cur = {k: v.clone() for k, v in vec.env_config().items()}

@@ -105,6 +105,57 @@ def test_onnx_reader_rejects_non_mlp():
         read_onnx(b"\x08\x08")  # a ModelProto without a graph
 
 
+def _independent():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_policy_fixture", GOLDEN / "make_policy_fixture.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_independent_decoder_agrees_on_synthetic_model():
+    """The fixture's decoder (tests/golden/make_policy_fixture.py, imports nothing from
+    swarm_marl_amd) and the product reader decode the same bytes to the same arrays."""
+    from swarm_marl_amd.onnx_weights import read_onnx
+    mod = _independent()
+    raw = synthetic_onnx(_random_layers(np.random.default_rng(3)))
+    nodes, arrays, gin, gout = mod.read_model(raw)
+    g = read_onnx(raw)
+    assert [n["op"] for n in nodes] == [n.op for n in g.nodes]
+    assert (gin, gout) == (g.inputs[0], g.outputs[0])
+    for name, arr in g.inits.items():
+        ind = arrays["init:" + name]
+        assert ind.dtype == arr.dtype and ind.shape == arr.shape and ind.tobytes() == arr.tobytes(), name
+
+
+def test_fixture_weights_match_product_reader_on_reference_artifact():
+    """Every initializer of the committed fixture (independent decode) equals, byte for byte,
+    what the product reader extracts from the reference's artifacts/policy.onnx — and so what
+    the GPU kernel is loaded with by PolicyMLP.from_onnx.  Needs /root/reference (build
+    container only)."""
+    from pathlib import Path
+    from swarm_marl_amd.onnx_weights import mlp_layers, read_onnx
+    src = Path("/root/reference/artifacts/policy.onnx")
+    if not src.exists():
+        pytest.skip("reference artifact not present (GPU box)")
+    d = np.load(GOLDEN / "policy_onnx.npz")
+    assert "independent" in str(d["decoder"])
+    g = read_onnx(src)
+    assert set("init:" + k for k in g.inits) == {k for k in d.files if k.startswith("init:")}
+    for name, arr in g.inits.items():
+        fx = d["init:" + name]
+        assert fx.dtype == arr.dtype and fx.shape == arr.shape and fx.tobytes() == arr.tobytes(), name
+    # and the Gemm chain the kernel runs is made of exactly those arrays
+    gem = [n for n in g.nodes if n.op == "Gemm"]
+    for (w, b, _), nd in zip(mlp_layers(g), gem):
+        assert w.tobytes() == d["init:" + nd.inputs[1]].tobytes()
+        assert b.tobytes() == d["init:" + nd.inputs[2]].tobytes()
+    # the independent decode of the artifact is the committed fixture's
+    _, arrays, _, _ = _independent().read_model(src.read_bytes())
+    for k, v in arrays.items():
+        assert v.tobytes() == d[k].tobytes(), k
+
+
 def test_policy_oracle_reproduces_fixture():
     from oracle.policy_oracle import eval_graph, load_fixture
     nodes, tensors, d = load_fixture(GOLDEN / "policy_onnx.npz")
