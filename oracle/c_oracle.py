@@ -6,12 +6,14 @@ bench.py's cpu_baseline leg (multi-threaded timing on the host cores).
 from __future__ import annotations
 
 import ctypes
+import os
 from pathlib import Path
 
 import numpy as np
 
 HERE = Path(__file__).resolve().parent
-LIB_PATH = HERE / "build" / "libswarm_oracle.so"
+# SWARM_ORACLE_LIB: another build of the same source (the ASan/UBSan one, tests/test_sanitizers_cpu.py)
+LIB_PATH = Path(os.environ.get("SWARM_ORACLE_LIB", HERE / "build" / "libswarm_oracle.so"))
 
 
 class Params(ctypes.Structure):  # mirror of swarm_params_t (include/swarm_mi355x.h)
