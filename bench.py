@@ -97,6 +97,8 @@ def parse(argv=None):
     ap.add_argument("--groups", type=int, default=None,
                     help="env groups per GPU, each stepped on its own HIP stream (VecSwarm groups=G); "
                          "default 2 for the headline and n256, 1 for n16")
+    ap.add_argument("--stagger-us", type=float, default=0.0,
+                    help="diagnostic: group 1's first timed step starts this much later (phase offset)")
     ap.add_argument("--gather-every", type=int, default=8,
                     help="CTDE all-gather period in steps (SURVEY.md §5: per batch, not per step)")
     ap.add_argument("--gs-slots", type=int, default=4,
@@ -403,6 +405,9 @@ def main(argv=None):
         def body():
             t_ev[0].record(stream)
             fork(t_ev[0])
+            if args.stagger_us > 0 and G > 1:  # diagnostic: start group 1 later (phase offset)
+                with torch.cuda.stream(vec.group_streams[1]):
+                    torch.cuda._sleep(int(args.stagger_us * 2400))
             if whole is not None:
                 replay_all(whole)
             else:

@@ -332,6 +332,17 @@ int swarm_eval_begin(const swarm_params_t* p, const swarm_eval_t* ev, const swar
  * step auto-reset).  Async on hip_stream, no allocation, no sync. */
 int swarm_eval_update(const swarm_params_t* p, const swarm_eval_t* ev, const swarm_out_t* out, void* hip_stream);
 
+/* Single-agent protocol (scripts/evaluate_protocol.py:193-234 `_run_single_episode_single_agent`
+ * over SingleDroneEnv): a batch of E single-drone envs (num_drones 1, neighbor_k 0, stepped with
+ * infos and auto_reset 0, ev->state_pos / state_goal set).  Unlike the swarm protocol the
+ * terminal step counts: its collision / reached_goal info and its position (the state, not yet
+ * reset).  Per env and step: reward sum, path length, first reached step, any collision; at
+ * terminated or truncated one record (formation_error 0) and reset_mask[e] = 1 (0 otherwise):
+ * the caller then runs swarm_reset(reset_mask) and swarm_eval_begin(reset_mask) — the next
+ * episode — without a host sync.  Replaces the reference's per-episode host loop. */
+int swarm_eval_single_update(const swarm_params_t* p, const swarm_eval_t* ev, const swarm_out_t* out,
+                             uint8_t* reset_mask, void* hip_stream);
+
 const char* swarm_eval_last_error(void);
 
 /*

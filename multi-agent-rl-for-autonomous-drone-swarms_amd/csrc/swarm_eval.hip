@@ -286,6 +286,58 @@ __global__ void __launch_bounds__(EVAL_THREADS * EVAL_WG_ENVS) eval_update_kerne
   v.status[e] = restarts ? SWARM_EVAL_LIVE : 0;
 }
 
+// Single-agent protocol (evaluate_protocol.py:193-234): one thread per env of single-drone envs.
+// The step ran without auto-reset, so the state still holds the terminal step's position; the
+// terminal step's info (collision, reached_goal) counts, which the swarm protocol never sees.
+__global__ void __launch_bounds__(256) eval_single_update_kernel(const EvalArgs a, uint8_t* __restrict__ reset_mask) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.E) return;
+  const swarm_eval_t& v = a.ev;
+  const uint8_t status = v.status[e];
+  const uint8_t done = a.env_done[e];
+  const uint8_t fl = a.info_flags[e];
+  const float rw = a.reward[e];
+  const float px = v.state_pos[3 * e], py = v.state_pos[3 * e + 1], pz = v.state_pos[3 * e + 2];
+  const float lx = v.last[3 * e], ly = v.last[3 * e + 1], lz = v.last[3 * e + 2];
+  const bool ends = (done & (SWARM_ENV_TERMINATED | SWARM_ENV_TRUNCATED)) != 0;
+  reset_mask[e] = (ends && (status & SWARM_EVAL_LIVE)) ? 1 : 0;
+  if (!(status & SWARM_EVAL_LIVE) || !(fl & SWARM_AGENT_STEPPED)) return;
+  const double ep_reward = v.ep_reward[e] + (double)rw;  // episode_reward += float(reward)
+  const double tr = v.traveled[e] + (double)norm1d(lx - px, ly - py, lz - pz);  // _distance(last, pos)
+  const int steps = v.ep_steps[e] + 1;
+  int reached = v.reached_step[e];
+  if ((fl & SWARM_AGENT_REACHED) && reached < 0) reached = steps;
+  const bool collided = (status & SWARM_EVAL_COLLIDED) || (fl & SWARM_AGENT_COLLISION);
+  if (!ends) {
+    v.ep_reward[e] = ep_reward;
+    v.traveled[e] = tr;
+    v.ep_steps[e] = steps;
+    v.reached_step[e] = reached;
+    v.last[3 * e] = px; v.last[3 * e + 1] = py; v.last[3 * e + 2] = pz;
+    if (collided) v.status[e] = status | SWARM_EVAL_COLLIDED;
+    return;
+  }
+  const float straight = norm1d(v.start[3 * e] - v.goal[3 * e], v.start[3 * e + 1] - v.goal[3 * e + 1],
+                                v.start[3 * e + 2] - v.goal[3 * e + 2]);
+  const long long genv = a.env_offset + e;
+  const unsigned seg = (unsigned)(genv % SWARM_EVAL_SEGMENTS);
+  const unsigned seg_cap = (unsigned)v.capacity / SWARM_EVAL_SEGMENTS;
+  const unsigned k = atomicAdd(v.count + seg, 1u);
+  if (k < seg_cap) {
+    double* rec = v.records + ((size_t)seg * seg_cap + k) * SWARM_EVAL_RECORD;
+    rec[0] = (double)genv;
+    rec[1] = (!collided && reached >= 0) ? 1.0 : 0.0;
+    rec[2] = collided ? 0.0 : 1.0;
+    rec[3] = reached >= 0 ? (double)reached : __builtin_nan("");
+    rec[4] = 0.0;  // formation_error: one agent
+    rec[5] = tr > 1e-8 ? (double)straight / tr : 0.0;
+    rec[6] = ep_reward;
+    rec[7] = (double)steps;
+    rec[8] = (double)v.update_index;
+  }
+  v.status[e] = 0;  // reopened by swarm_eval_begin after the caller's reset
+}
+
 thread_local char g_eerr[256] = "";
 int efail(int code, const char* fmt, ...) {
   va_list ap;
@@ -351,6 +403,25 @@ int swarm_eval_update(const swarm_params_t* p, const swarm_eval_t* ev, const swa
                      (hipStream_t)hip_stream, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? SWARM_OK : efail(SWARM_EHIP, "eval_update launch: %s", hipGetErrorString(e));
+}
+
+int swarm_eval_single_update(const swarm_params_t* p, const swarm_eval_t* ev, const swarm_out_t* o,
+                             uint8_t* reset_mask, void* hip_stream) {
+  EvalArgs a;
+  const int rc = make_args(p, ev, o, &a);
+  if (rc) return rc;
+  if (p->num_drones != 1 || p->neighbor_k > 0)
+    return efail(SWARM_EINVAL, "the single-agent protocol needs num_drones 1 and neighbor_k 0 (SingleDroneEnv)");
+  if (p->auto_reset) return efail(SWARM_EINVAL, "the single-agent protocol needs auto_reset 0 (terminal positions)");
+  if (!ev->state_pos) return efail(SWARM_ENULL, "state_pos / state_goal are required by the single-agent protocol");
+  if (!o->reward || !o->info_flags || !o->env_done)
+    return efail(SWARM_ENULL, "out.reward/info_flags/env_done required (build the env with infos)");
+  if (!reset_mask) return efail(SWARM_ENULL, "reset_mask is NULL");
+  if (a.E == 0) return SWARM_OK;
+  hipLaunchKernelGGL(eval_single_update_kernel, dim3((a.E + 255) / 256), dim3(256), 0, (hipStream_t)hip_stream, a,
+                     reset_mask);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? SWARM_OK : efail(SWARM_EHIP, "eval_single_update launch: %s", hipGetErrorString(e));
 }
 
 const char* swarm_eval_last_error(void) { return g_eerr; }

@@ -1558,9 +1558,12 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   const size_t ea = (size_t)env * S64_N;  // first agent of the env (uniform)
   float* __restrict__ const soa = reinterpret_cast<float*>(ring + S64_N);  // S64Lds::w.soa
   S64ArgPtr A = s64_args();  // re-fetched at every phase boundary
-  STAMP_AT(env, 0);
 #ifdef SWARM_STAMPS
-  if ((threadIdx.x & 63) == 0 && env < (1 << 16)) g_stamps[env * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+  const int srec = env + (int)A->P.env_offset;  // stamp record: the global env (env groups)
+#endif
+  STAMP_AT(srec, 0);
+#ifdef SWARM_STAMPS
+  if ((threadIdx.x & 63) == 0 && srec < (1 << 16)) g_stamps[srec * 16 + 11] = __builtin_amdgcn_s_memrealtime();
 #endif
 
   // ---- inputs (prefetched): env-uniform scalars, per-lane rows, obstacles to LDS
@@ -1577,7 +1580,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   float* __restrict__ const osoa = reinterpret_cast<float*>(obst + S64_MMAX);  // S64Lds::w.osoa
   if (t < M) s64_put_obst(obst, osoa, t, c.ox, c.oy, c.oz);
   const int n_active = __popcll(__ballot(act));
-  STAMP_AT(env, 1);
+  STAMP_AT(srec, 1);
 
   // ---- integrate: drone_swarm_env.py:98-117 (identical to swarm_kernel, DYN_KIN) or the
   // point-mass physics substeps (identical to swarm_kernel, DYN_PHYS)
@@ -1652,7 +1655,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   wave_sync();
   prefetch();  // `c` is dead from here on
   if constexpr (SWARM_PRIO_MODE >= 2) __builtin_amdgcn_s_setprio(1);
-  STAMP_AT(env, 2);
+  STAMP_AT(srec, 2);
   A = s64_args();
 
   // ---- pair + obstacle passes
@@ -1688,7 +1691,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     obstacle_pass_s64<MSL, true>(osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
   }
   if constexpr (LANDED) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next env's inputs are in
-  STAMP_AT(env, 3);
+  STAMP_AT(srec, 3);
   A = s64_args();
 
   // ---- exact top-K (finish_keys, rare exact_select)
@@ -1702,7 +1705,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     if (slow_nb) exact_select<KS, false>(ring, S64_N, t, S64_K, max_first(wd, S64_K), px, py, pz, wd, wj);
     if (slow_ob) exact_select<MSL, true>(obst, M, -1, S64_MS, max_first(od, S64_MS), px, py, pz, od, oj);
   };
-  STAMP_AT(env, 4);
+  STAMP_AT(srec, 4);
 
   // ---- rewards / terminations: drone_swarm_env.py:120-172
   // The pair collision comes from the nearest key, not from the exact top-K: the finish runs
@@ -1796,7 +1799,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     A->O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
                                 (do_reset ? SWARM_ENV_RESET : 0u));
   const uint64_t m_term = __ballot(term), m_trunc = __ballot(trunc);
-  STAMP_AT(env, 5);
+  STAMP_AT(srec, 5);
   A = s64_args();
 
   // ---- in-kernel auto-reset (wave-uniform): new episode, then its key passes
@@ -1847,7 +1850,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     select_topk(DYN == DYN_KIN);  // the kinematic step pass ranks by d~, physics by s'
   }
 
-  STAMP_AT(env, 6);
+  STAMP_AT(srec, 6);
   A = s64_args();
   // ---- state write-back
   const bool new_act = do_reset || (DYN == DYN_PHYS ? (act && !(term_all || trunc_all)) : cont);
@@ -1892,7 +1895,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     if (t == 0) { gs[6 * S64_N + 0] = gx; gs[6 * S64_N + 1] = gy; gs[6 * S64_N + 2] = gz; }
   }
 
-  STAMP_AT(env, 7);
+  STAMP_AT(srec, 7);
   A = s64_args();
   // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)] (drone_swarm_env.py:226-291)
   float row[D];
@@ -1982,12 +1985,12 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     if (NR && t < NR) store_obs(A->O.obs + ea * D, S64_N * D * 4, 16u * (ch * V4 + t + 64 * NF), v[NF]);
     wave_sync();
   }
-  STAMP_AT(env, 8);
+  STAMP_AT(srec, 8);
 #ifdef SWARM_STAMPS
-  if ((threadIdx.x & 63) == 0 && env < (1 << 16)) {
-    g_stamps[env * 16 + 9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
-    g_stamps[env * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-    g_stamps[env * 16 + 12] = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0 && srec < (1 << 16)) {
+    g_stamps[srec * 16 + 9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+    g_stamps[srec * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    g_stamps[srec * 16 + 12] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
 }
@@ -2011,7 +2014,17 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
 #ifndef SWARM_PRIO_MODE
 #define SWARM_PRIO_MODE 0
 #endif
+#ifndef SWARM_GROUP_PRIO
+#define SWARM_GROUP_PRIO 0
+#endif
 __device__ __forceinline__ void s64_set_priority() {
+  if constexpr (SWARM_GROUP_PRIO > 0) {
+    // diagnostic: env groups alternate priority (group g starts at env_offset = g * E_g), so the
+    // two groups' compute phases do not share the SIMDs' issue evenly
+    S64ArgPtr A = s64_args();
+    const long long q = A->P.E > 0 ? A->P.env_offset / A->P.E : 0;
+    if ((q & 1) == 0) __builtin_amdgcn_s_setprio(SWARM_GROUP_PRIO);
+  }
   if constexpr (SWARM_PRIO_LEVELS > 1) {
     const int lvl = (int)((blockIdx.x >> 3) % SWARM_PRIO_LEVELS) * 3 / (SWARM_PRIO_LEVELS - 1);
     switch (lvl) {

@@ -60,7 +60,8 @@ EXPORTED_SYMBOLS = (
     "swarm_abi_version", "swarm_last_error", "swarm_params_default", "swarm_obs_dim",
     "swarm_query_launch", "swarm_step", "swarm_reset", "swarm_observe",
     "swarm_policy_packed_bytes", "swarm_policy_pack", "swarm_policy_forward", "swarm_policy_last_error",
-    "swarm_eval_begin", "swarm_eval_update", "swarm_eval_last_error", "swarm_env_cfg_set",
+    "swarm_eval_begin", "swarm_eval_update", "swarm_eval_single_update", "swarm_eval_last_error",
+    "swarm_env_cfg_set",
 )
 ENV_CFG_BYTES = 64  # sizeof(swarm_env_cfg_t)
 
@@ -203,6 +204,8 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.swarm_eval_begin.argtypes = [P, ev, O, vp, vp]
     lib.swarm_eval_update.restype = ctypes.c_int
     lib.swarm_eval_update.argtypes = [P, ev, O, vp]
+    lib.swarm_eval_single_update.restype = ctypes.c_int
+    lib.swarm_eval_single_update.argtypes = [P, ev, O, vp, vp]
     lib.swarm_eval_last_error.restype = ctypes.c_char_p
     lib.swarm_eval_last_error.argtypes = []
     lib.swarm_env_cfg_set.restype = ctypes.c_int

@@ -150,3 +150,41 @@ class EvalTracker:
 
     def clear(self) -> None:
         self.count.zero_()
+
+
+class SingleAgentEvalTracker(EvalTracker):
+    """scripts/evaluate_protocol.py:193-234 (`_run_single_episode_single_agent`) for E
+    single-drone envs at once — the SingleDroneEnv protocol, on the device:
+
+        vec = VecSwarm(E, cfg, num_drones=1, with_infos=True, auto_reset=False)  # cfg neighbor_k=0
+        vec.reset(); ev = SingleAgentEvalTracker(vec); ev.begin()
+        for t in range(T):
+            vec.step(policy(vec.obs)); ev.update()   # closes episodes, resets and reopens those envs
+        ev.aggregate()
+
+    Unlike the swarm protocol the terminal step's info and position count (SingleDroneEnv emits
+    them), so SR = 0 / CFR = 0 / NaN TTG episodes occur.  The env must not auto-reset (the
+    terminal position must still be in the state): `update()` runs swarm_eval_single_update,
+    which closes the finished episodes and flags them, then swarm_reset and swarm_eval_begin of
+    exactly those envs — three launches, no host sync."""
+
+    def __init__(self, vec: VecSwarm, capacity: int = 65536):
+        if vec.num_drones != 1 or int(vec.cfg.neighbor_k) != 0:
+            raise ValueError("SingleAgentEvalTracker needs a single-drone VecSwarm (num_drones=1, neighbor_k=0)")
+        if int(vec.params.auto_reset):
+            raise ValueError("SingleAgentEvalTracker needs auto_reset=False (it resets the finished envs itself)")
+        if vec.groups != 1:
+            raise ValueError("SingleAgentEvalTracker runs on one env group")
+        super().__init__(vec, capacity)
+        self.reset_mask = torch.zeros(vec.num_envs, dtype=torch.uint8, device=vec.device)
+
+    def update(self) -> None:
+        """Accumulate the last step; finished episodes are recorded, reset and reopened."""
+        v = self.vec
+        self.updates += 1
+        self._c.update_index = self.updates
+        nat.check(self.lib.swarm_eval_single_update(ctypes.byref(v._gparams[0]), ctypes.byref(self._c),
+                                                    ctypes.byref(v._gout[0]), self.reset_mask.data_ptr(),
+                                                    self._stream()), self.lib, which="eval")
+        v.reset(env_mask=self.reset_mask)
+        self.begin(env_mask=self.reset_mask)

@@ -6,11 +6,14 @@ dict outputs of an env step loop, the per-episode summary of
   * :103-116  formation error of a set of positions (mean over agents of the mean |d_ij - d*|),
   * :237-331  `_run_single_episode_multi_agent`: success, collision-free, time-to-goal,
               formation error, path efficiency, episode reward,
+  * :193-234  `_run_single_episode_single_agent` (SingleDroneEnv: the terminal step's info and
+              position count; formation error 0),
   * :334-350  `_aggregate` over episodes,
 including the reference's behaviour that an agent without an observation contributes neither a
 collision nor a "not reached" vote: on the terminal step (no observations at all,
 drone_swarm_env.py:154) the all-reached test passes vacuously.  Pinned by
-tests/golden/eval_*.npz (generated from the reference by tests/golden/make_eval_golden.py).
+tests/golden/eval_*.npz and eval1_*.npz (generated from the reference by
+tests/golden/make_eval_golden.py).
 """
 from __future__ import annotations
 
@@ -86,6 +89,56 @@ class EpisodeMetrics:
                 float(self.reached_step) if self.reached_step is not None else math.nan,
                 float(np.mean(self.fe)) if self.fe else 0.0, float(np.mean(pe)) if pe else 0.0,
                 float(self.reward))
+
+
+class SingleEpisodeMetrics:
+    """evaluate_protocol.py:193-234 restated: one SingleDroneEnv episode from its reset
+    observation and the (obs, reward, terminated, truncated, info) of every step."""
+
+    def __init__(self, reset_obs):
+        o = np.asarray(reset_obs, np.float32)
+        self.start = o[0:3].copy()
+        self.goal = self.start + o[6:9]  # float32: start + goal vector, as the reference
+        self.last = self.start.copy()
+        self.traveled = 0.0
+        self.reward = 0.0
+        self.steps = 0
+        self.reached_step = None
+        self.collided = False
+
+    def update(self, obs, reward, terminated, truncated, info) -> bool:
+        self.steps += 1
+        self.reward += float(reward)
+        p = np.asarray(obs, np.float32)[0:3]
+        self.traveled += distance(self.last, p)
+        self.last = p.copy()
+        if bool(info.get("collision", False)):
+            self.collided = True
+        if bool(info.get("reached_goal", False)) and self.reached_step is None:
+            self.reached_step = self.steps
+        return bool(terminated or truncated)
+
+    def summary(self) -> tuple:
+        straight = distance(self.start, self.goal)
+        pe = straight / self.traveled if self.traveled > 1e-8 else 0.0
+        return (int((not self.collided) and self.reached_step is not None), int(not self.collided),
+                float(self.reached_step) if self.reached_step is not None else math.nan, 0.0, float(pe),
+                float(self.reward))
+
+
+def single_drone_step(env, action):
+    """SingleDroneEnv.step (single_drone_env.py:73-111) through the per-agent swarm restatement
+    with one drone and no neighbours (oracle/swarm_loop.LoopSwarm, pinned to the reference
+    fixtures, single_drone.npz included): same integrator, reward terms and flags; unlike the
+    swarm dict API it returns the terminal step's observation and info."""
+    i = 0
+    _, rew, _, _, _ = env.step({env.ids[i]: action})
+    after = env._goal_dist(i)
+    at_goal = after <= env.c["goal_radius"]
+    hit = i in env._hits([i])
+    obs = env.observe(i)
+    info = {"distance_to_goal": after, "reached_goal": bool(at_goal), "collision": bool(hit)}
+    return obs, rew[env.ids[i]], bool(at_goal or hit), bool(env.t >= env.c["max_steps"]), info
 
 
 def aggregate(summaries) -> dict:

@@ -27,11 +27,11 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
-from make_golden import DroneSwarmEnv  # noqa: E402  (gymnasium stand-in + reference import)
+from make_golden import DroneSwarmEnv, SingleDroneEnv  # noqa: E402  (gymnasium stand-in + reference import)
 
 EVAL_SCRIPT = "/root/reference/scripts/evaluate_protocol.py"
 WANTED = ("EpisodeSummary", "_safe_std", "_distance", "_formation_error_from_positions",
-          "_run_single_episode_multi_agent", "_aggregate")
+          "_run_single_episode_multi_agent", "_run_single_episode_single_agent", "_aggregate")
 
 
 def load_metric_functions() -> dict:
@@ -43,6 +43,7 @@ def load_metric_functions() -> dict:
     exec("import math\nimport numpy as np\nfrom dataclasses import dataclass\nfrom typing import Any\n"
          "from statistics import mean, pstdev\n", ns)
     ns["DroneSwarmEnv"] = DroneSwarmEnv
+    ns["SingleDroneEnv"] = SingleDroneEnv
     exec(compile(mod, EVAL_SCRIPT, "exec"), ns)
     return ns
 
@@ -116,6 +117,52 @@ def run_case(fns, name: str, cfg: dict, episodes: int, seed: int, noise: float) 
     print(f"{name}: {episodes} episodes, lengths {lens.tolist()}, {os.path.getsize(path)} B, agg {agg}")
 
 
+def run_case_single(fns, name: str, cfg: dict, episodes: int, seed: int, noise: float) -> None:
+    """evaluate_protocol.py:193-234 `_run_single_episode_single_agent` over the reference
+    SingleDroneEnv: unlike the swarm protocol it sees the terminal step's info (collision,
+    reached_goal) and position, so SR = 0, CFR = 0 and NaN TTG all occur."""
+    env = SingleDroneEnv(dict(cfg))
+    resets, actions, summaries = [], [], []
+    orig_reset, orig_step = env.reset, env.step
+    cur = {}
+
+    def reset(*, seed=None, options=None):
+        out = orig_reset(seed=seed, options=options)
+        resets.append(dict(pos=env.position.copy(), goal=env.goal.copy(), obst=env.obstacles.copy()))
+        cur["acts"] = []
+        return out
+
+    def step(action):
+        cur["acts"].append(np.asarray(action, np.float32).reshape(3))
+        return orig_step(action)
+
+    env.reset, env.step = reset, step
+    algo = RecordingAlgo(env, seed, noise)
+    for _ in range(episodes):
+        s = fns["_run_single_episode_single_agent"](algo, env)
+        summaries.append([s.success, s.collision_free, s.time_to_goal, s.formation_error,
+                          s.path_efficiency, s.episode_reward])
+        actions.append(np.stack(cur["acts"]))
+    agg = fns["_aggregate"]([fns["EpisodeSummary"](*[type(f)(v) for f, v in zip((0, 0, 0.0, 0.0, 0.0, 0.0), row)])
+                             for row in summaries])
+    lens = np.array([len(a) for a in actions], np.int32)
+    act = np.zeros((episodes, int(lens.max()), 3), np.float32)
+    for k in range(episodes):
+        act[k, :lens[k]] = actions[k]
+    sm = np.array(summaries, np.float64)
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, config=json.dumps(cfg), lengths=lens, actions=act,
+                        reset_pos=np.stack([r["pos"] for r in resets]),
+                        reset_goal=np.stack([r["goal"] for r in resets]),
+                        reset_obst=np.stack([r["obst"] for r in resets]),
+                        summaries=sm,
+                        summary_fields=np.array(["success", "collision_free", "time_to_goal",
+                                                 "formation_error", "path_efficiency", "episode_reward"]),
+                        aggregate=json.dumps(agg))
+    print(f"{name}: {episodes} episodes, lengths {lens.tolist()}, success {sm[:, 0].tolist()}, "
+          f"collision_free {sm[:, 1].tolist()}, {os.path.getsize(path)} B, agg {agg}")
+
+
 def main() -> None:
     fns = load_metric_functions()
     run_case(fns, "eval_n4", {"num_drones": 4, "seed": 11, "max_steps": 120}, 6, seed=1, noise=0.6)
@@ -123,6 +170,10 @@ def main() -> None:
              seed=2, noise=0.3)
     run_case(fns, "eval_n3_obst0", {"num_drones": 3, "seed": 13, "max_steps": 200, "num_obstacles": 0}, 5,
              seed=3, noise=0.2)
+    # single-agent protocol: goal reached, obstacle collisions and time-limit episodes
+    run_case_single(fns, "eval1_obst", {"seed": 21, "max_steps": 60, "num_obstacles": 12, "obstacle_radius": 1.6},
+                    12, seed=4, noise=0.35)
+    run_case_single(fns, "eval1_tl", {"seed": 22, "max_steps": 18, "num_obstacles": 6}, 8, seed=5, noise=1.2)
 
 
 if __name__ == "__main__":

@@ -9,7 +9,7 @@ import numpy as np
 GOLDEN = Path(__file__).resolve().parent / "golden"
 
 ROLLOUT_FIXTURES = sorted(p.name for p in GOLDEN.glob("*.npz")
-                          if not p.name.startswith(("reset_", "single", "policy_", "eval_")))
+                          if not p.name.startswith(("reset_", "single", "policy_", "eval")))
 
 
 def load_fixture(name: str):

@@ -63,6 +63,55 @@ def test_eval_oracle_matches_reference(name):
         assert (isinstance(v, float) and math.isnan(v) and math.isnan(agg[key])) or agg[key] == pytest.approx(v, rel=1e-12), key
 
 
+EVAL1_FIXTURES = sorted(p.name for p in GOLDEN.glob("eval1_*.npz"))
+
+
+def single_env(d, cfg, k):
+    """LoopSwarm with one drone and no neighbours at recorded episode k's reset state."""
+    from oracle.swarm_loop import LoopSwarm
+    raw = dict(cfg)
+    raw.pop("seed", None)
+    env = LoopSwarm(1, neighbor_k=0, **raw)
+    env.pos = d["reset_pos"][k].reshape(1, 3).copy()
+    env.vel = np.zeros((1, 3), np.float32)
+    env.goal = d["reset_goal"][k].copy()
+    env.obst = d["reset_obst"][k].copy()
+    env.live, env.t = [0], 0
+    return env
+
+
+@pytest.mark.parametrize("name", EVAL1_FIXTURES)
+def test_single_agent_eval_oracle_matches_reference(name):
+    """evaluate_protocol.py:193-234 over the reference SingleDroneEnv (eval1_*.npz): goal
+    reached, collision (SR = CFR = 0) and time-limit (NaN TTG) episodes."""
+    from oracle import eval_oracle as ev
+    d = np.load(GOLDEN / name)
+    cfg = json.loads(str(d["config"]))
+    sums = []
+    for k in range(len(d["lengths"])):
+        env = single_env(d, cfg, k)
+        m = ev.SingleEpisodeMetrics(env.observe(0))
+        n = int(d["lengths"][k])
+        for t in range(n):
+            done = m.update(*ev.single_drone_step(env, d["actions"][k, t]))
+            assert done == (t == n - 1), (name, k, t)
+        s = m.summary()
+        for f, (a, b) in enumerate(zip(s, d["summaries"][k])):
+            assert (math.isnan(a) and math.isnan(b)) or a == pytest.approx(b, rel=1e-12, abs=1e-12), (name, k, f)
+        sums.append(s)
+    agg = ev.aggregate(sums)
+    for key, v in json.loads(str(d["aggregate"])).items():
+        assert (isinstance(v, float) and math.isnan(v) and math.isnan(agg[key])) or agg[key] == pytest.approx(v, rel=1e-12), key
+
+
+def test_single_agent_fixtures_cover_failure_branches():
+    """The eval1 fixtures hold successes, collisions and time-limit episodes (the branches the
+    swarm protocol's fixtures cannot reach)."""
+    sm = np.concatenate([np.load(GOLDEN / n)["summaries"] for n in EVAL1_FIXTURES])
+    assert (sm[:, 0] == 1).any() and (sm[:, 0] == 0).any()
+    assert (sm[:, 1] == 0).any() and np.isnan(sm[:, 2]).any()
+
+
 # ---------------------------------------------------------------- curriculum / aggregation host logic
 STAGES = {"promotion_window_episodes": 4, "stages": [
     {"stage_id": 1, "stage_name": "a", "env_config": {"num_drones": 3, "num_obstacles": 0, "max_steps": 30},

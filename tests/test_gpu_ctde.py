@@ -10,6 +10,7 @@ bit, a synchronous join-then-gather of a single-stream, single-buffer run of the
 """
 from __future__ import annotations
 
+import json
 import os
 import socket
 
@@ -88,7 +89,6 @@ def test_overlapped_gather_equals_synchronous(pg, e, n, groups, slots, every):
 def test_bench_ctde_rehearsal_line_one_rank(pg, capsys):
     """bench.main's CTDE branch end to end on one rank (RCCL group of one): the gather runs every
     --gather-every steps inside the timed region and the line says so."""
-    import json
     import bench
     bench_args = ["--config", "n256", "--envs", "64", "--steps", "16", "--warmup", "2",
                   "--device-warmup-ms", "0", "--no-cpu-baseline", "--gather-every", "4"]

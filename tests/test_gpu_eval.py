@@ -134,3 +134,61 @@ def test_curriculum_runner_stages(dev):
         assert m["episodes"] > 0 and 0.0 <= m["success_rate"] <= 1.0
         run.advance()
     assert seen == [(3, 0), (5, 4)]
+
+
+EVAL1_FIXTURES = sorted(p.name for p in GOLDEN.glob("eval1_*.npz"))
+
+
+@pytest.mark.parametrize("name", EVAL1_FIXTURES)
+def test_single_agent_eval_replays_reference_episodes(dev, name):
+    """evaluate_protocol.py:193-234 over the reference SingleDroneEnv (eval1_*.npz, made by the
+    reference's own function): each recorded episode is one single-drone env of a VecSwarm from
+    its recorded reset state and actions, stepped by the HIP kernel and measured by
+    swarm_eval_single_update.  The fixtures hold goal-reached, collision (SR = CFR = 0) and
+    time-limit (NaN TTG) episodes; the terminal step's info and position count."""
+    from swarm_marl_amd import VecSwarm
+    from swarm_marl_amd.eval_metrics import SingleAgentEvalTracker
+    d = np.load(GOLDEN / name)
+    cfg = dict(json.loads(str(d["config"])), neighbor_k=0)
+    lens = d["lengths"]
+    e = len(lens)
+    vec = VecSwarm(e, cfg, num_drones=1, device=dev, auto_reset=False, with_infos=True, seed=77)
+    vec.set_state(pos=d["reset_pos"].reshape(e, 1, 3), vel=np.zeros((e, 1, 3), np.float32), goal=d["reset_goal"],
+                  obstacles=d["reset_obst"], active=np.ones((e, 1), bool), step_count=np.zeros(e, np.int32))
+    vec.observe()
+    ev = SingleAgentEvalTracker(vec, capacity=4096)
+    ev.begin()
+    acts = torch.as_tensor(d["actions"], device=dev)  # [episodes, T, 3]
+    for t in range(int(lens.max())):
+        a = acts[:, t].reshape(e, 1, 3).contiguous()
+        vec.step(a)
+        ev.update()  # finished envs are reset on the device and start new (unrecorded) episodes
+    rec = ev.records()
+    first = {}
+    for row in rec:  # completion order: the first record of each env is the recorded episode
+        first.setdefault(int(row[0]), row)
+    assert sorted(first) == list(range(e))
+    sm = d["summaries"]
+    for k in range(e):
+        row = first[k]
+        assert int(row[7]) == int(lens[k]), (name, k)
+        _cmp_summary(row, sm[k], int(lens[k]), (name, k))
+    got = [first[k] for k in range(e)]
+    from swarm_marl_amd.eval_metrics import aggregate_records
+    agg, ref = aggregate_records(np.stack(got)), json.loads(str(d["aggregate"]))
+    for key in ("success_rate", "collision_free_rate"):
+        assert agg[key] == ref[key], key
+    assert (math.isnan(agg["mean_time_to_goal"]) and math.isnan(ref["mean_time_to_goal"])) or \
+        agg["mean_time_to_goal"] == ref["mean_time_to_goal"]
+    assert agg["path_efficiency"] == pytest.approx(ref["path_efficiency"], rel=1e-9)
+    assert (sm[:, 0] == 0).any() or (sm[:, 1] == 0).any()  # the failure branches are exercised
+
+
+def test_single_agent_eval_rejects_swarm_batches(dev):
+    from swarm_marl_amd import VecSwarm
+    from swarm_marl_amd.eval_metrics import SingleAgentEvalTracker
+    with pytest.raises(ValueError):
+        SingleAgentEvalTracker(VecSwarm(4, {"num_drones": 3}, device=dev, auto_reset=False, with_infos=True))
+    with pytest.raises(ValueError):
+        SingleAgentEvalTracker(VecSwarm(4, {"neighbor_k": 0}, num_drones=1, device=dev, auto_reset=True,
+                                        with_infos=True))

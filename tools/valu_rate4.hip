@@ -29,6 +29,33 @@ KERNEL(k_pkfma, INIT, "v_pk_fma_f32 v[14:15], v[8:9], v[10:11], v[8:9]", CL)
 KERNEL(k_dpp, INIT, "v_add_f32_dpp v14, v8, v9 wave_ror:1 row_mask:0xf bank_mask:0xf", CL)
 KERNEL(k_cndmask, INIT, "v_cndmask_b32 v14, v8, v9, vcc", CL)
 KERNEL(k_sqrtf64, INIT, "v_sqrt_f64 v[14:15], v[8:9]", CL)
+KERNEL(k_minf, INIT, "v_min_f32 v14, v8, v9", CL)
+KERNEL(k_maxf, INIT, "v_max_f32 v14, v8, v9", CL)
+KERNEL(k_med3f, INIT, "v_med3_f32 v14, v8, v9, v10", CL)
+KERNEL(k_min3f, INIT, "v_min3_f32 v14, v8, v9, v10", CL)
+KERNEL(k_minu, INIT, "v_min_u32 v14, v12, v13", CL)
+KERNEL(k_fmaf, INIT, "v_fma_f32 v14, v8, v9, v10", CL)
+KERNEL(k_mulf, INIT, "v_mul_f32 v14, v8, v9", CL)
+KERNEL(k_subf, INIT, "v_sub_f32 v14, v8, v9", CL)
+KERNEL(k_addabs, INIT, "v_add_f32_e64 v14, |v8|, v9", CL)
+KERNEL(k_andor, INIT, "v_and_or_b32 v14, v12, v13, v8", CL)
+KERNEL(k_and, INIT, "v_and_b32 v14, v12, v13", CL)
+KERNEL(k_or, INIT, "v_or_b32 v14, v12, v13", CL)
+KERNEL(k_bfi, INIT, "v_bfi_b32 v14, v12, v13, v8", CL)
+KERNEL(k_addu, INIT, "v_add_u32 v14, v12, v13", CL)
+KERNEL(k_xor, INIT, "v_xor_b32 v14, v12, v13", CL)
+KERNEL(k_mov, INIT, "v_mov_b32 v14, v12", CL)
+KERNEL(k_cmpf, INIT, "v_cmp_lt_f32 vcc, v8, v9", CL)
+KERNEL(k_cnd64, INIT, "v_cndmask_b32_e64 v14, v8, v9, s[20:21]", CL)
+KERNEL(k_cvtfi, INIT, "v_cvt_f32_u32 v14, v12", CL)
+KERNEL(k_pkmul, INIT, "v_pk_mul_f32 v[14:15], v[8:9], v[10:11]", CL)
+KERNEL(k_fmac, INIT, "v_fmac_f32 v14, v8, v9", CL)
+KERNEL(k_ldexp, INIT, "v_ldexp_f32 v14, v8, v12", CL)
+KERNEL(k_mulhif, INIT, "v_mul_hi_u32_u24 v14, v12, v13", CL)
+KERNEL(k_lshl, INIT, "v_lshlrev_b32 v14, 2, v12", CL)
+KERNEL(k_addf_dep, INIT, "v_add_f32 v14, v14, v9", CL)
+KERNEL(k_med3u_dep, INIT, "v_med3_u32 v14, v14, v13, v8", CL)
+KERNEL(k_med3f_dep, INIT, "v_med3_f32 v14, v14, v9, v10", CL)
 
 int main() {
   float* out;
@@ -38,7 +65,14 @@ int main() {
       {"v_mul_hi_u32", k_mulhi}, {"v_mul_lo_u32", k_mullo}, {"v_mul_u32_u24", k_mul24},
       {"v_add_f64", k_addf64}, {"v_fma_f64", k_fmaf64}, {"v_cvt_f64_f32", k_cvtf64}, {"v_cvt_f32_f64", k_cvtf32},
       {"v_med3_u32", k_med3u}, {"v_pk_add_f32", k_pkadd}, {"v_pk_fma_f32", k_pkfma}, {"v_add_f32_dpp", k_dpp},
-      {"v_cndmask_b32", k_cndmask}, {"v_sqrt_f64", k_sqrtf64}};
+      {"v_cndmask_b32", k_cndmask}, {"v_sqrt_f64", k_sqrtf64},
+      {"v_min_f32", k_minf}, {"v_max_f32", k_maxf}, {"v_med3_f32", k_med3f}, {"v_min3_f32", k_min3f},
+      {"v_min_u32", k_minu}, {"v_fma_f32", k_fmaf}, {"v_mul_f32", k_mulf}, {"v_sub_f32", k_subf},
+      {"v_add_f32 |a|", k_addabs}, {"v_and_or_b32", k_andor}, {"v_and_b32", k_and}, {"v_or_b32", k_or},
+      {"v_bfi_b32", k_bfi}, {"v_add_u32", k_addu}, {"v_xor_b32", k_xor}, {"v_mov_b32", k_mov},
+      {"v_cmp_lt_f32", k_cmpf}, {"v_cndmask_e64 s", k_cnd64}, {"v_cvt_f32_u32", k_cvtfi}, {"v_pk_mul_f32", k_pkmul},
+      {"v_fmac_f32", k_fmac}, {"v_ldexp_f32", k_ldexp}, {"v_mul_hi_u32_u24", k_mulhif}, {"v_lshlrev_b32", k_lshl},
+      {"v_add_f32 dep", k_addf_dep}, {"v_med3_u32 dep", k_med3u_dep}, {"v_med3_f32 dep", k_med3f_dep}};
   const int blocks = 256 * 8;  // 8 waves per SIMD at 4 waves per workgroup
   hipEvent_t a, b;
   hipEventCreate(&a);
