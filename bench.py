@@ -97,6 +97,13 @@ def parse(argv=None):
     ap.add_argument("--groups", type=int, default=None,
                     help="env groups per GPU, each stepped on its own HIP stream (VecSwarm groups=G); "
                          "default 2 for the headline and n256, 1 for n16")
+    ap.add_argument("--graph", choices=("split", "fused"), default="split",
+                    help="env groups in the timed hipGraph: one graph per group stream, or one graph "
+                         "holding every group's chain (fork/join captured)")
+    ap.add_argument("--warm-graph", choices=("whole", "ring"), default="whole",
+                    help="device warm-up replays the timed K-step graph (whole) or the 8-step ring graphs")
+    ap.add_argument("--split-reset", action="store_true",
+                    help="diagnostic: after each group launch, swarm_reset of the envs it reset (timing only)")
     ap.add_argument("--stagger-us", type=float, default=0.0,
                     help="diagnostic: group 1's first timed step starts this much later (phase offset)")
     ap.add_argument("--gather-every", type=int, default=8,
@@ -310,6 +317,13 @@ def main(argv=None):
     G = vec.groups
     slices = vec.group_slices
 
+    import ctypes
+
+    def split_reset(g):  # diagnostic (--split-reset): the group's reset envs by swarm_reset
+        lo = slices[g][0]
+        vec.lib.swarm_reset(ctypes.byref(vec._gparams[g]), ctypes.byref(vec._gstate[g]),
+                            vec.env_done.data_ptr() + lo, ctypes.byref(vec._gout[g]), vec._stream())
+
     def env_step_group(g, k):  # group g's step k on the current stream
         if pol is not None:  # rollout: actions from the policy on the current obs, in place
             lo, hi = slices[g]
@@ -317,6 +331,8 @@ def main(argv=None):
             vec.step_group(g, pol_act)
         else:
             vec.step_group(g, ring[k % args.ring])
+        if args.split_reset:
+            split_reset(g)
 
     def env_step(k):  # whole batch: group g on group stream g (not joined: groups overlap)
         if G == 1:
@@ -385,26 +401,49 @@ def main(argv=None):
                             env_step_group(g, k)
                 out.append(gr)
             return out
+        def capture_fused(n_steps):  # ONE graph holding every group's chain (fork / join inside)
+            gr = torch.cuda.CUDAGraph()
+            s0 = vec.group_streams[0]
+            with torch.cuda.stream(s0), torch.cuda.graph(gr, stream=s0, capture_error_mode="thread_local"):
+                ev_f = torch.cuda.Event()
+                ev_f.record(s0)
+                for st in vec.group_streams[1:]:
+                    st.wait_event(ev_f)
+                for k in range(n_steps):
+                    for g, st in enumerate(vec.group_streams):
+                        with torch.cuda.stream(st):
+                            env_step_group(g, k)
+                for st in vec.group_streams[1:]:
+                    ev_j = torch.cuda.Event()
+                    ev_j.record(st)
+                    s0.wait_event(ev_j)
+            return [gr]
+
+        fused = args.graph == "fused" and G > 1
         graphs = capture(args.ring)
-        # short timed regions (the driver's K = 20) replay all K steps from one graph per group,
-        # so that the wall clock holds one graph launch per group; longer ones replay ring
-        # segments plus a graph of the K % ring remainder
-        whole = capture(args.steps) if args.steps <= 256 else None
+        # short timed regions (the driver's K = 20) replay all K steps from one graph per group
+        # (or one fused graph), so that the wall clock holds one graph launch per group; longer
+        # ones replay ring segments plus a graph of the K % ring remainder
+        whole = ((capture_fused if fused else capture)(args.steps)) if args.steps <= 256 else None
         tail = capture(rem) if rem and whole is None else None
 
         def replay_all(gs):
-            if G == 1:
-                gs[0].replay()
+            if G == 1 or len(gs) == 1:  # one group, or the fused graph (on group stream 0)
+                with torch.cuda.stream(stream if G == 1 else vec.group_streams[0]):
+                    gs[0].replay()
                 return
             for g, st in enumerate(vec.group_streams):
                 with torch.cuda.stream(st):
                     gs[g].replay()
         replay_all(graphs)  # untimed
+        if whole is not None:
+            replay_all(whole)  # untimed: the timed region is not the graph's first launch
         sync()
 
         def body():
             t_ev[0].record(stream)
-            fork(t_ev[0])
+            if not (fused and whole is not None):
+                fork(t_ev[0])
             if args.stagger_us > 0 and G > 1:  # diagnostic: start group 1 later (phase offset)
                 with torch.cuda.stream(vec.group_streams[1]):
                     torch.cuda._sleep(int(args.stagger_us * 2400))
@@ -415,11 +454,13 @@ def main(argv=None):
                     replay_all(graphs)
                 if tail is not None:
                     replay_all(tail)
-            join()
+            if not (fused and whole is not None):
+                join()
             t_ev[1].record(stream)
         timing = (f"hipGraph replay of the {args.steps} steps (actions from a {args.ring}-tensor ring)"
                   if whole is not None else f"hipGraph replay of {args.ring}-step segments") + (
-            f", {G} env groups on {G} HIP streams (one graph per group)" if G > 1 else "") + (
+            (f", {G} env groups on {G} HIP streams (" + ("one graph holding all groups" if fused and whole is not None
+                                                        else "one graph per group") + ")") if G > 1 else "") + (
             f" (policy {args.policy} + env step per step)" if pol is not None else "")
     else:
         def body():
@@ -443,8 +484,12 @@ def main(argv=None):
         while ((time.perf_counter() - t0) * 1e3 < args.device_warmup_ms if fixed is None
                else warm_steps < fixed):
             if use_graph:
-                replay_all(graphs)
-                warm_steps += args.ring
+                if whole is not None and args.warm_graph == "whole":
+                    replay_all(whole)
+                    warm_steps += args.steps
+                else:
+                    replay_all(graphs)
+                    warm_steps += args.ring
             else:
                 for k in range(args.ring):
                     step(k)

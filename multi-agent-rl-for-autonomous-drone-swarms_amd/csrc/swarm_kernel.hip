@@ -63,6 +63,7 @@
 #define ABL_ROW_ONLY 512    // step64: obs row computed, neither staged nor stored
 #define ABL_RESET_WORK 1024 // step64: a resetting env draws its new state but skips its key passes,
                             // finish and obs (wrong obs; the dynamics are unchanged)
+#define ABL_EXACT 2048      // sqrt_rn = v_sqrt_f32 and the sdot norm in f32 (inexact; timing only)
 
 // Diagnostic phase timestamps (tools/stamps.py; never set in the product build)
 #ifdef SWARM_STAMPS
@@ -145,6 +146,7 @@ __device__ __forceinline__ int clamp_obstacles(int m, int M) { return m < 0 ? 0 
 // The fast path is OCML's own correction step without its input scaling (needed only below
 // 2^-96) and special-value fixup (inf/NaN/negative never occur here): bit-identical results.
 __device__ __forceinline__ float sqrt_rn(float x) {
+  if (SWARM_ABLATE & ABL_EXACT) return __builtin_amdgcn_sqrtf(x);
   if (__builtin_expect(__ballot(!(x >= 0x1p-96f || x == 0.0f)) != 0, 0)) return __builtin_sqrtf(x);
   float r = __builtin_amdgcn_sqrtf(x);  // v_sqrt_f32, within 1 ulp
   const float rm = __uint_as_float(__float_as_uint(r) - 1u), rp = __uint_as_float(__float_as_uint(r) + 1u);
@@ -158,6 +160,7 @@ __device__ __forceinline__ double dsqrt_rn(double x) { return __builtin_sqrt(x);
 // products, rounded to float.  Returns the float sum s; the norm is sqrt_rn(s).
 __device__ __forceinline__ float sqsum_1d(float x, float y, float z) {
   const float xx = x * x, yy = y * y, zz = z * z;
+  if (SWARM_ABLATE & ABL_EXACT) return (xx + yy) + zz;
   return (float)(((double)xx + (double)yy) + (double)zz);
 }
 // np.linalg.norm(A, axis=1): float32 ((x*x)+(y*y))+(z*z).
@@ -1445,11 +1448,20 @@ __device__ __forceinline__ void obstacle_pass_s64(const float* __restrict__ os, 
                                                   bool chk, float s_thr, uint32_t keep,
                                                   uint32_t (&ok)[MSL > 0 ? MSL : 1], bool& coll) {
   int m = 0;
+  // software pipelined: pair m+2's planes are read while pair m is ranked (index clamped into
+  // the 16-entry planes; the stale values of a pair past M are never used)
+  s64_f2 X = {os[0], os[1]};
+  s64_f2 Y = {os[S64_MMAX], os[S64_MMAX + 1]};
+  s64_f2 Z = {os[2 * S64_MMAX], os[2 * S64_MMAX + 1]};
   for (; m + 1 < M; m += 2) {
-    const s64_f2 X = {os[m], os[m + 1]};
-    const s64_f2 Y = {os[S64_MMAX + m], os[S64_MMAX + m + 1]};
-    const s64_f2 Z = {os[2 * S64_MMAX + m], os[2 * S64_MMAX + m + 1]};
+    const int n = m + 2 < S64_MMAX - 1 ? m + 2 : S64_MMAX - 2;
+    const s64_f2 Xn = {os[n], os[n + 1]};
+    const s64_f2 Yn = {os[S64_MMAX + n], os[S64_MMAX + n + 1]};
+    const s64_f2 Zn = {os[2 * S64_MMAX + n], os[2 * S64_MMAX + n + 1]};
     const s64_f2 dx = X - px, dy = Y - py, dz = Z - pz;
+    X = Xn;
+    Y = Yn;
+    Z = Zn;
     const s64_f2 sq = (dx * dx + dy * dy) + dz * dz;
     if constexpr (MSL > 0) {
       kins<MSL>(ok, (__float_as_uint(sq.x) & keep) | (uint32_t)m);
@@ -1478,6 +1490,58 @@ __device__ __forceinline__ void s64_put(float4* __restrict__ ring, float* __rest
     soa[t + S64_N] = px; soa[S64_SOA + t + S64_N] = py; soa[2 * S64_SOA + t + S64_N] = pz;
     soa[3 * S64_SOA + t + S64_N] = w;
   }
+}
+
+// step64's finish in the common case, straight-line: N = 64 > K and M >= Ms fill every survivor
+// slot, so finish_keys' per-slot validity branches (which serialise the nine exact-distance
+// chains into separate basic blocks) are not needed.  The first K neighbour and Ms obstacle
+// survivors get their exact distances as independent chains; the answer is finish_keys' own
+// whenever no two survivors are a near-tie and the survivor bound holds.  Returns false for a
+// lane that needs the general finish (finish_keys + exact_select); the caller runs that for the
+// whole wave when any lane does (its answer for the other lanes is the same).
+template <int KS, int MSL>
+__device__ __forceinline__ bool s64_finish_fast(const uint32_t (&nk)[KS], const uint32_t (&ok)[MSL],
+                                                const float4* __restrict__ ring, const float4* __restrict__ obst,
+                                                int t, int M, uint32_t nb_keep, uint32_t ob_keep, bool dkey,
+                                                float px, float py, float pz, float (&wd)[KS], int (&wj)[KS],
+                                                float (&od)[MSL], int (&oj)[MSL]) {
+  constexpr int K = KS - 1, MS = MSL - 1;
+  const uint32_t nim = ~nb_keep, oim = ~ob_keep;
+  bool near = false;
+#pragma unroll
+  for (int s = 0; s + 1 < KS; ++s)
+    near = near | (__uint_as_float(nk[s + 1] & nb_keep) <= __uint_as_float((nk[s] & nb_keep) | nim) * FAST_HI);
+#pragma unroll
+  for (int s = 0; s + 1 < MSL; ++s)
+    near = near | ((ok[s + 1] != KEY_EMPTY) &
+                   (__uint_as_float(ok[s + 1] & ob_keep) <= __uint_as_float((ok[s] & ob_keep) | oim) * FAST_HI));
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    const int j = (t + (int)(nk[s] & nim)) & (S64_N - 1);
+    const float4 q = ring[j];
+    wd[s] = sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
+    wj[s] = j;
+  }
+  wd[K] = __builtin_inff();
+  wj[K] = 0x7fffffff;
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    const int j = (int)(ok[s] & oim);
+    const float4 q = obst[j & (S64_MMAX - 1)];
+    od[s] = sqrt_rn(sqsum_f(q.x - px, q.y - py, q.z - pz));
+    oj[s] = j;
+  }
+  od[MS] = __builtin_inff();
+  oj[MS] = 0x7fffffff;
+  // survivor bounds (finish_keys' tails: APPROX neighbour keys, exact obstacle keys)
+  const float nb_base = __uint_as_float(nk[K] & nb_keep) * FAST_LO;
+  const float w = wd[K - 1];
+  const bool ok_nb = dkey ? nb_base > w : nb_base > (w * w) * FAST_HI;
+  const uint32_t last = ok[MS];
+  const float wo = od[MS - 1];
+  const bool ok_ob = last == KEY_EMPTY || (int)(last & oim) >= M ||
+                     __uint_as_float(last & ob_keep) > (wo * wo) * FAST_HI;
+  return !near && ok_nb && ok_ob;
 }
 
 // One env's inputs, loaded one env ahead of its compute (software pipeline): raw loaded values
@@ -1688,7 +1752,12 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     if (fast) pair_pass_s64<KS, 1, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
 #endif
     else pair_pass_s64<KS, 1, false>(soa, t, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
-    obstacle_pass_s64<MSL, true>(osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
+    if (SWARM_ABLATE & ABL_OBST) {  // diagnostic: obstacle collisions only, no obstacle keys
+      uint32_t ok0[1];
+      obstacle_pass_s64<0, true>(osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok0, ocoll);
+    } else {
+      obstacle_pass_s64<MSL, true>(osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
+    }
   }
   if constexpr (LANDED) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next env's inputs are in
   STAMP_AT(srec, 3);
@@ -1698,6 +1767,16 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   float wd[KS], od[MSL];
   int wj[KS], oj[MSL];
   auto select_topk = [&](bool dkey) {
+    if (SWARM_ABLATE & ABL_FINISH) {  // diagnostic: the keys as the answer (wrong distances)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) { wd[s] = __uint_as_float(nk[s] & A->P.nb_keep); wj[s] = (int)(nk[s] & 63u) + t; }
+#pragma unroll
+      for (int s = 0; s < MSL; ++s) { od[s] = __uint_as_float(ok[s] & A->P.ob_keep); oj[s] = (int)(ok[s] & 15u); }
+      return;
+    }
+    if (__ballot(!s64_finish_fast<KS, MSL>(nk, ok, ring, obst, t, M, A->P.nb_keep, A->P.ob_keep, dkey, px, py, pz, wd,
+                                           wj, od, oj)) == 0)
+      return;
     const bool slow_nb = !finish_keys<KS, false, true>(nk, ring, S64_N, t, S64_N - 1, S64_K, A->P.nb_keep, dkey, px, py,
                                                        pz, wd, wj);
     const bool slow_ob = !finish_keys<MSL, true, false>(ok, obst, M, 0, 0x7fffffff, S64_MS, A->P.ob_keep, false, px, py,
@@ -1843,7 +1922,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       float s2 = 0.f;
       double f2 = 0.0;
       pair_pass_s64<KS, 0, true>(soa, t, px, py, pz, true, A->P.nb_keep, 0.f, nk, s2, f2);
-      obstacle_pass_s64<MSL, false>(osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
+      if (!(SWARM_ABLATE & ABL_OBST)) obstacle_pass_s64<MSL, false>(osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
       select_topk(false);
     }
   } else {
