@@ -63,6 +63,8 @@ extern "C" {
 #define SWARM_KERNEL_STEP64_PERSISTENT 2  /* swarm_step64: the same step on a persistent grid of
                                    waves_per_simd waves per SIMD with per-XCD env queues
                                    (E > grid; needs state.work, else STEP64 is launched) */
+#define SWARM_KERNEL_STEP16Q 3  /* swarm_step16q: N = 16, K = 3, Ms = 4, 4 <= M <= 16, kinematic step; one
+                                   env per 64-lane wave, four lanes per drone (BASELINE config 2) */
 
 /* env_done bits ([E] u8) */
 #define SWARM_ENV_TERMINATED 1u  /* terminated["__all__"] */

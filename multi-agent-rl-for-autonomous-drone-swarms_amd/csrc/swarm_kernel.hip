@@ -40,7 +40,8 @@
 
 // Build partitioning: the kernel instantiations are compiled as parallel translation units.
 // SWARM_PART k in 0..3 holds the kernels of (KIND, DYN) = (k >> 1, k & 1); SWARM_PART 4 holds
-// the host side and the C-ABI; SWARM_PART 5 the headline specialisation swarm_step64;
+// the host side and the C-ABI; SWARM_PART 5 the headline specialisation swarm_step64; SWARM_PART 6
+// the config-2 specialisation swarm_step16q;
 // SWARM_PART -1 (default) is everything in one unit (tools/).
 #ifndef SWARM_PART
 #define SWARM_PART -1
@@ -2188,7 +2189,15 @@ swarm_step64(const S64Args args) {
     if (head != nullptr && t == 0) v = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return v;
   };
+#ifdef SWARM_S64_STATIC  // diagnostic: static stride assignment instead of the env queues
+  head = nullptr;
+  env = blockIdx.x;
+#endif
   auto settle = [&](uint32_t v) -> int {
+#ifdef SWARM_S64_STATIC
+    (void)v;
+    return env + (int)gridDim.x < A->P.E ? env + (int)gridDim.x : -1;
+#endif
     if (head == nullptr) return -1;
     v = __builtin_amdgcn_readfirstlane(v);
     if (v == n_draws - 1u && t == 0) __hip_atomic_store(head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2213,6 +2222,430 @@ swarm_step64(const S64Args args) {
     env = nxt;
   }
   if (!first) settle(ticket);
+}
+
+// ------------------------------------------------------------------ step16q: config 2 (N = 16)
+// BASELINE config 2 (N = 16 drones x E = 1024 envs) is a latency-bound launch: 1,024 envs of
+// 16 drones fill a quarter of the SIMDs even as one env per wave, so the step time is the
+// instruction latency of one wave, not the chip's throughput.  This specialisation puts one env
+// in each 64-lane wave with FOUR lanes per drone (lane l = 4 d + q) and splits the per-drone work
+// across the quarter q:
+//  * pair pass: drone d's 15 partners are the symmetric rotations r = 1 .. 8 (r < 8 with a mirror
+//    to drone d + r by ds_bpermute, r = 8 evaluated from both sides); quarter q takes r = q + 1
+//    and q + 5, so a lane ranks 3-4 candidates instead of 15; the four partial top-4 lists are
+//    merged across the quad with two DPP bitonic merges (12 min/max each), formation partial sums
+//    and running minima with two DPP reductions;
+//  * finish: quarter q computes the exact distance of neighbour slot q and obstacle slot q;
+//  * observation row: quarter q stores its slots' 4-float groups, quarter 3 also p, v, g - p,
+//    straight from registers (no LDS stage: the launch is latency-bound).
+// Integrate, obstacle pass, rewards and terminations run redundantly on the four lanes of a
+// drone (identical values); every per-drone output is written by quarter 0.  Same numerics as
+// swarm_kernel<0, 0, 4, 5, 1> (the generic kernel at N = 16), obs bit-identical
+// (tests/test_gpu_step16.py).  Kinematic step, K = 3, Ms = 4, 4 <= M <= 16, no per-env records.
+constexpr int Q_N = 16;
+constexpr int Q_K = 3;
+constexpr int Q_MS = 4;
+constexpr int Q_D = 9 + 4 * Q_K + 4 * Q_MS;  // 37
+constexpr int Q_MMAX = 16;
+constexpr uint64_t Q_LEAD = 0x1111111111111111ull;  // quarter 0 of every drone
+constexpr int Q_WG_ENVS = 4;                        // independent one-env waves per workgroup
+
+struct Q16Lds {
+  float soa[4 * 32];  // x, y, z, eligibility planes; drone j at j and j + 16
+  float4 ring[Q_N];
+  float4 obst[Q_MMAX];
+  float osoa[3 * Q_MMAX];
+};
+
+// DPP quad permutations: xor 1, xor 2, broadcast of quad lane k
+__device__ __forceinline__ uint32_t quad_xor1(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ uint32_t quad_xor2(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false); }
+template <int K>
+__device__ __forceinline__ float quad_bcast(float v) {
+  constexpr int ctrl = K | (K << 2) | (K << 4) | (K << 6);
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xF, 0xF, false));
+}
+// Merge this lane's ascending 4-key list with the partner lane's (quad xor X): the 4 smallest of
+// the union, ascending (bitonic: min(a_i, b_3-i), then a 4-element bitonic sort).
+template <int X>
+__device__ __forceinline__ void quad_merge4(uint32_t (&k)[4]) {
+  uint32_t b[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) b[i] = X == 1 ? quad_xor1(k[i]) : quad_xor2(k[i]);
+  uint32_t c[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c[i] = min(k[i], b[3 - i]);
+  const uint32_t c0 = min(c[0], c[2]), c2 = max(c[0], c[2]);
+  const uint32_t c1 = min(c[1], c[3]), c3 = max(c[1], c[3]);
+  k[0] = min(c0, c1); k[1] = max(c0, c1);
+  k[2] = min(c2, c3); k[3] = max(c2, c3);
+}
+__device__ __forceinline__ float quad_sum(float v) {
+  v = v + __uint_as_float(quad_xor1(__float_as_uint(v)));
+  return v + __uint_as_float(quad_xor2(__float_as_uint(v)));
+}
+__device__ __forceinline__ float quad_min(float v) {
+  v = fminf(v, __uint_as_float(quad_xor1(__float_as_uint(v))));
+  return fminf(v, __uint_as_float(quad_xor2(__float_as_uint(v))));
+}
+
+// One quarter's share of the symmetric pair pass of drone d: rotations q + 1 and q + 5 (r = 8 has
+// no mirror).  PASS 1: d~ keys + formation + running minimum (non-FAST); PASS 0: s' keys only.
+template <int PASS, bool FAST>
+__device__ __forceinline__ void q16_pair_pass(const float* __restrict__ soa, int d, int q, float px, float py, float pz,
+                                              bool self, uint32_t keep, float ds, uint32_t (&nk)[4], float& smin,
+                                              float& esum) {
+  const uint32_t sflag = (FAST || self) ? 0u : 0x80000000u;
+  const uint32_t keep_m = keep & 0x7fffffffu;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int r = q + 1 + 4 * it;
+    const int j = d + r;  // ring index (wrap copy at j + 16)
+    const float s = sqsum_rank(soa[j] - px, soa[32 + j] - py, soa[64 + j] - pz);
+    const float v = PASS == 1 ? __builtin_amdgcn_sqrtf(s) : s;
+    const bool el = FAST || (self && soa[96 + j] != 0.f);
+    kins<4>(nk, (__float_as_uint(v) & keep) | (uint32_t)r);
+    if constexpr (PASS == 1) {
+      if constexpr (!FAST) smin = fminf(smin, el ? v : __builtin_inff());
+      esum += el ? fabsf(v - ds) : 0.f;
+    }
+    // mirror: lane (d, q) receives drone (d - r)'s value of the pair (d - r, d) from lane 4(d - r) + q
+    const int src = (((d - r) & (Q_N - 1)) << 2) | q;
+    const uint32_t rcv = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)(__float_as_uint(v) | sflag));
+    if (r < 8) {
+      const float vm = __uint_as_float(rcv & 0x7fffffffu);
+      const bool pr = FAST || (self && !(rcv >> 31));
+      kins<4>(nk, (rcv & keep_m) | (uint32_t)(Q_N - r));
+      if constexpr (PASS == 1) {
+        if constexpr (!FAST) smin = fminf(smin, pr ? vm : __builtin_inff());
+        esum += pr ? fabsf(vm - ds) : 0.f;
+      }
+    }
+  }
+  quad_merge4<1>(nk);
+  quad_merge4<2>(nk);
+  if constexpr (PASS == 1) {
+    esum = quad_sum(esum);
+    if constexpr (!FAST) smin = quad_min(smin);
+  }
+}
+
+template <int G>
+__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(8)))
+swarm_step16q(const S64Args args) {
+  (void)args;  // read through s64_args()
+  constexpr int KS = Q_K + 1, MSL = Q_MS + 1;
+  __shared__ Q16Lds ldsq[G];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  S64ArgPtr A = s64_args();
+  const int env = blockIdx.x * G + w;
+  if (env >= A->P.E) return;  // whole wave
+  Q16Lds& L = ldsq[w];
+  const int d = lane >> 2, q = lane & 3;
+  STAMP_AT(env, 0);
+#ifdef SWARM_STAMPS
+  if (lane == 0 && env < (1 << 16)) g_stamps[env * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+#endif
+  const int M = A->P.M;
+  const size_t ea = (size_t)env * Q_N;
+  const size_t ag = ea + d;
+  // ---- loads (the four lanes of a drone read the same words)
+  uint32_t gse = 0u;
+  {
+    const uint32_t* src = lane < 3 ? reinterpret_cast<const uint32_t*>(A->S.goal) + 3 * env + lane
+                                   : (lane == 3 ? reinterpret_cast<const uint32_t*>(A->S.step_count) + env
+                                                : A->S.episode + env);
+    if (lane < 5) gse = *src;
+  }
+  float ax = A->actions[ag * 3], ay = A->actions[ag * 3 + 1], az = A->actions[ag * 3 + 2];
+  float px = A->S.pos[ag * 3], py = A->S.pos[ag * 3 + 1], pz = A->S.pos[ag * 3 + 2];
+  float vx = A->S.vel[ag * 3], vy = A->S.vel[ag * 3 + 1], vz = A->S.vel[ag * 3 + 2];
+  bool act = A->S.active[ag] != 0;
+  const bool has = A->amask == nullptr || A->amask[ag] != 0;
+  if (lane < M) {
+    const float* o = A->S.obstacles + ((size_t)env * M + lane) * 3;
+    const float ox = o[0], oy = o[1], oz = o[2];
+    L.obst[lane] = make_float4(ox, oy, oz, 0.f);
+    L.osoa[lane] = ox; L.osoa[Q_MMAX + lane] = oy; L.osoa[2 * Q_MMAX + lane] = oz;
+  }
+  float gx = __uint_as_float(__builtin_amdgcn_readlane(gse, 0));
+  float gy = __uint_as_float(__builtin_amdgcn_readlane(gse, 1));
+  float gz = __uint_as_float(__builtin_amdgcn_readlane(gse, 2));
+  const int stepc = (int)__builtin_amdgcn_readlane(gse, 3);
+  const uint32_t episode0 = (uint32_t)__builtin_amdgcn_readlane(gse, 4);
+  const int n_active = __popcll(__ballot(act) & Q_LEAD);
+  STAMP_AT(env, 1);
+  A = s64_args();
+
+  // ---- integrate: drone_swarm_env.py:98-117 (swarm_kernel, DYN_KIN)
+  float prev_d = 0.f;
+  if (act) {
+    prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
+    if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
+    ax = clampf(ax, -1.f, 1.f) * A->P.amax;
+    ay = clampf(ay, -1.f, 1.f) * A->P.amax;
+    az = clampf(az, -1.f, 1.f) * A->P.amax;
+    vx = vx + ax * A->P.dt;
+    vy = vy + ay * A->P.dt;
+    vz = vz + az * A->P.dt;
+    const float s_sp = sqsum_1d(vx, vy, vz);
+    if (!(s_sp <= A->P.s_vmax)) {
+      const float sp = sqrt_rn(s_sp);
+      if (!(sp <= A->P.vmax || sp < (float)1e-8)) {
+        vx = (vx / sp) * A->P.vmax;
+        vy = (vy / sp) * A->P.vmax;
+        vz = (vz / sp) * A->P.vmax;
+      }
+    }
+    px = px + vx * A->P.dt;
+    py = py + vy * A->P.dt;
+    pz = pz + vz * A->P.dt;
+  }
+  if (n_active > 0) {
+    px = clampf(px, A->P.neg_half_w, A->P.half_w);
+    py = clampf(py, A->P.neg_half_w, A->P.half_w);
+    pz = clampf(pz, A->P.neg_half_w, A->P.half_w);
+  }
+  auto put = [&](float w_el) {
+    if (q == 0) {
+      L.ring[d] = make_float4(px, py, pz, w_el);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        L.soa[d + 16 * c] = px; L.soa[32 + d + 16 * c] = py; L.soa[64 + d + 16 * c] = pz;
+        L.soa[96 + d + 16 * c] = w_el;
+      }
+    }
+  };
+  put(act ? 1.f : 0.f);
+  wave_sync();
+  STAMP_AT(env, 2);
+  A = s64_args();
+
+  // ---- pair + obstacle passes
+  uint32_t nk[KS], ok[MSL];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
+#pragma unroll
+  for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
+  float smin = __builtin_inff(), esum = 0.f;
+  bool ocoll = false;
+  const bool fast = (__ballot(act) & Q_LEAD) == Q_LEAD;
+  if (fast) q16_pair_pass<1, true>(L.soa, d, q, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, esum);
+  else q16_pair_pass<1, false>(L.soa, d, q, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, esum);
+  obstacle_pass_s64<MSL, true>(L.osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
+  STAMP_AT(env, 3);
+  A = s64_args();
+
+  // ---- rewards / terminations: drone_swarm_env.py:120-172 (swarm_kernel, DYN_KIN)
+  bool pcoll;
+  if (fast) {
+    const uint32_t keep = A->P.nb_keep;
+    pcoll = __uint_as_float(nk[0] | ~keep) * FAST_HI <= A->P.thr_pair;
+    if (!pcoll && __uint_as_float(nk[0] & keep) * FAST_LO <= A->P.thr_pair)
+      pcoll = key_zero_hit<true>(nk[0], keep, A->P.s_pair) || exact_pair_collision(L.ring, Q_N, d, px, py, pz, A->P.s_pair);
+  } else {
+    pcoll = smin <= A->P.thr_pair * FAST_LO;
+    if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act)
+      pcoll = exact_pair_collision(L.ring, Q_N, d, px, py, pz, A->P.s_pair);
+  }
+  const float curr = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
+  float rew = 0.f;
+  bool reached = false, collided = false, term = false, trunc = false, cont = false;
+  bool term_all = false, trunc_all = false;
+  int new_step = stepc;
+  if (act) {
+    reached = (double)curr <= A->P.goal_radius;
+    collided = ocoll || pcoll;
+    double r = ((double)prev_d - (double)curr) * A->P.kp;
+    if (n_active > 1) r = r + (-A->P.kf) * ((double)esum * inv_count(n_active - 1));
+    if (reached) r = r + A->P.r_goal;
+    if (collided) r = r + A->P.r_col;
+    rew = (float)r;
+  }
+  const bool any_c = (__ballot(act && collided) & Q_LEAD) != 0;
+  const bool any_cand = (__ballot(act && !reached && !collided) & Q_LEAD) != 0;
+  if (n_active == 0) {
+    term_all = true;
+  } else {
+    new_step = stepc + 1;
+    const bool tl = new_step >= A->P.max_steps;
+    term_all = (!any_cand && !any_c && !tl) || any_c;
+    trunc_all = tl && !term_all;
+    if (act) {
+      const bool done_i = reached || collided;
+      term = done_i;
+      trunc = tl && !done_i;
+      cont = !done_i && !tl && !any_c;
+    }
+  }
+  const bool do_reset = A->P.auto_reset && (term_all || trunc_all);
+  if (q == 0) {
+    A->O.reward[ag] = rew;
+    if (A->O.dist_goal) A->O.dist_goal[ag] = curr;
+    if (A->O.info_flags)
+      A->O.info_flags[ag] = (uint8_t)((act ? SWARM_AGENT_STEPPED : 0u) | (act && reached ? SWARM_AGENT_REACHED : 0u) |
+                                      (act && collided ? SWARM_AGENT_COLLISION : 0u) | (cont ? SWARM_AGENT_HAS_OBS : 0u));
+  }
+  if (lane == 0)
+    A->O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
+                                   (do_reset ? SWARM_ENV_RESET : 0u));
+  const uint64_t m_term = __ballot(term), m_trunc = __ballot(trunc);
+  STAMP_AT(env, 4);
+  A = s64_args();
+
+  // ---- in-kernel auto-reset (wave-uniform): new episode, then its key passes
+  uint32_t episode_new = episode0;
+  bool dkey = true;
+  if (do_reset) {
+    const long long genv = A->P.env_offset + env;
+    episode_new = episode0 + 1u;
+    uint32_t wd4[4], wo[4];
+    draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)d, wd4);
+    draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)(Q_N + (lane < M ? lane : M)), wo);
+    const float lo_w = A->P.neg_half_w, wd_w = A->P.width_w;
+    px = uni(wd4[0], lo_w, wd_w);
+    py = uni(wd4[1], lo_w, wd_w);
+    pz = uni(wd4[2], lo_w, wd_w);
+    vx = vy = vz = 0.f;
+    act = true;
+    const float ox = uni(wo[0], lo_w, wd_w), oy = uni(wo[1], lo_w, wd_w), oz = uni(wo[2], lo_w, wd_w);
+    wave_sync();  // every read of the old ring / obstacles is done
+    if (lane < M) {
+      L.obst[lane] = make_float4(ox, oy, oz, 0.f);
+      L.osoa[lane] = ox; L.osoa[Q_MMAX + lane] = oy; L.osoa[2 * Q_MMAX + lane] = oz;
+    }
+    gx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ox), M));
+    gy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(oy), M));
+    gz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(oz), M));
+    put(1.f);
+    wave_sync();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
+#pragma unroll
+    for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
+    float s2 = 0.f, e2 = 0.f;
+    bool c2 = false;
+    q16_pair_pass<0, true>(L.soa, d, q, px, py, pz, true, A->P.nb_keep, 0.f, nk, s2, e2);
+    obstacle_pass_s64<MSL, false>(L.osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
+    dkey = false;  // PASS 0 ranks by s'
+  }
+  STAMP_AT(env, 5);
+  A = s64_args();
+
+  // ---- exact top-K: quarter q finishes neighbour slot q (q < 3) and obstacle slot q
+  const uint32_t nim = ~A->P.nb_keep, oim = ~A->P.ob_keep;
+  float nd = 0.f, ndx = 0.f, ndy = 0.f, ndz = 0.f, od = 0.f, odx = 0.f, ody = 0.f, odz = 0.f;
+  {
+    bool near = false;
+#pragma unroll
+    for (int s = 0; s + 1 < KS; ++s)
+      near = near | (__uint_as_float(nk[s + 1] & A->P.nb_keep) <=
+                     __uint_as_float((nk[s] & A->P.nb_keep) | nim) * FAST_HI);
+#pragma unroll
+    for (int s = 0; s + 1 < MSL; ++s)
+      near = near | ((ok[s + 1] != KEY_EMPTY) & (__uint_as_float(ok[s + 1] & A->P.ob_keep) <=
+                                                 __uint_as_float((ok[s] & A->P.ob_keep) | oim) * FAST_HI));
+    // this quarter's slots (q = 3 has no neighbour slot: it repeats slot 2, unused)
+    const uint32_t kn = q == 0 ? nk[0] : (q == 1 ? nk[1] : nk[2]);
+    const int jn = (d + (int)(kn & nim)) & (Q_N - 1);
+    const float4 qn = L.ring[jn];
+    ndx = qn.x - px; ndy = qn.y - py; ndz = qn.z - pz;
+    nd = sqrt_rn(sqsum_1d(ndx, ndy, ndz));
+    const uint32_t ko = q == 0 ? ok[0] : (q == 1 ? ok[1] : (q == 2 ? ok[2] : ok[3]));
+    const int jo = (int)(ko & oim) & (Q_MMAX - 1);
+    const float4 qo = L.obst[jo];
+    odx = qo.x - px; ody = qo.y - py; odz = qo.z - pz;
+    od = sqrt_rn(sqsum_f(odx, ody, odz));
+    // survivor bounds (finish_keys' tails) with slot K-1 / Ms-1 from quarters 2 / 3
+    const float w2 = quad_bcast<2>(nd), w3 = quad_bcast<3>(od);
+    const float nb_base = __uint_as_float(nk[Q_K] & A->P.nb_keep) * FAST_LO;
+    const bool ok_nb = dkey ? nb_base > w2 : nb_base > (w2 * w2) * FAST_HI;
+    const uint32_t last = ok[Q_MS];
+    const bool ok_ob = last == KEY_EMPTY || (int)(last & oim) >= M ||
+                       __uint_as_float(last & A->P.ob_keep) > (w3 * w3) * FAST_HI;
+    if (__ballot(near || !ok_nb || !ok_ob) != 0) {
+      // rare: the general finish on every lane (near-ties, unproven bounds), quarter q keeps its slots
+      float wd[KS], odv[MSL];
+      int wj[KS], oj[MSL];
+      const bool slow_nb = !finish_keys<KS, false, true>(nk, L.ring, Q_N, d, Q_N - 1, Q_K, A->P.nb_keep, dkey, px, py,
+                                                         pz, wd, wj);
+      const bool slow_ob = !finish_keys<MSL, true, false>(ok, L.obst, M, 0, 0x7fffffff, Q_MS, A->P.ob_keep, false, px,
+                                                          py, pz, odv, oj);
+      if (slow_nb) exact_select<KS, false>(L.ring, Q_N, d, Q_K, max_first(wd, Q_K), px, py, pz, wd, wj);
+      if (slow_ob) exact_select<MSL, true>(L.obst, M, -1, Q_MS, max_first(odv, Q_MS), px, py, pz, odv, oj);
+      const int sn = q < 2 ? q : 2;
+      nd = sn == 0 ? wd[0] : (sn == 1 ? wd[1] : wd[2]);
+      const int jn2 = (sn == 0 ? wj[0] : (sn == 1 ? wj[1] : wj[2])) & (Q_N - 1);
+      const float4 qn2 = L.ring[jn2];
+      ndx = qn2.x - px; ndy = qn2.y - py; ndz = qn2.z - pz;
+      od = q == 0 ? odv[0] : (q == 1 ? odv[1] : (q == 2 ? odv[2] : odv[3]));
+      const int jo2 = (q == 0 ? oj[0] : (q == 1 ? oj[1] : (q == 2 ? oj[2] : oj[3]))) & (Q_MMAX - 1);
+      const float4 qo2 = L.obst[jo2];
+      odx = qo2.x - px; ody = qo2.y - py; odz = qo2.z - pz;
+    }
+  }
+  STAMP_AT(env, 6);
+  A = s64_args();
+
+  // ---- state write-back (quarter 0), byte rows from ballots, env scalars (lane 0)
+  const bool new_act = do_reset || cont;
+  if (q == 0) {
+    float* pe = A->S.pos + ag * 3;
+    float* ve = A->S.vel + ag * 3;
+    pe[0] = px; pe[1] = py; pe[2] = pz;
+    ve[0] = vx; ve[1] = vy; ve[2] = vz;
+  }
+  {
+    const uint64_t m_act = __ballot(new_act);
+    uint8_t* p_term = A->O.terminated;
+    uint8_t* p_trunc = A->O.truncated;
+    uint8_t* p_act = A->S.active;
+    asm volatile("" : "+s"(p_term), "+s"(p_trunc), "+s"(p_act));
+    const int grp = lane >> 2;  // lanes 0-3 terminated, 4-7 truncated, 8-11 active: dword lane & 3
+    if (grp < 3) {
+      const uint64_t m = grp == 0 ? m_term : (grp == 1 ? m_trunc : m_act);
+      const uint32_t nib = (uint32_t)(m >> (16 * (lane & 3)));  // drones 4k .. 4k+3 at bits 0, 4, 8, 12
+      const uint32_t word = (nib & 1u) | ((nib >> 4) & 1u) << 8 | ((nib >> 8) & 1u) << 16 | ((nib >> 12) & 1u) << 24;
+      uint8_t* base = grp == 0 ? p_term : (grp == 1 ? p_trunc : p_act);
+      *reinterpret_cast<uint32_t*>(base + ea + 4 * (lane & 3)) = word;
+    }
+  }
+  if (lane == 0) {
+    A->S.step_count[env] = do_reset ? 0 : new_step;
+    if (do_reset) {
+      A->S.episode[env] = episode_new;
+      A->S.goal[3 * env + 0] = gx; A->S.goal[3 * env + 1] = gy; A->S.goal[3 * env + 2] = gz;
+    }
+  }
+  if (do_reset && lane < M) {
+    float* o = A->S.obstacles + ((size_t)env * M + lane) * 3;
+    const float4 qo = L.obst[lane];
+    o[0] = qo.x; o[1] = qo.y; o[2] = qo.z;
+  }
+  if (A->O.global_state && q == 0) {
+    float* gs = A->O.global_state + (size_t)env * (6 * Q_N + 3);
+    gs[3 * d] = px; gs[3 * d + 1] = py; gs[3 * d + 2] = pz;
+    gs[3 * Q_N + 3 * d] = vx; gs[3 * Q_N + 3 * d + 1] = vy; gs[3 * Q_N + 3 * d + 2] = vz;
+    if (d == 0) { gs[6 * Q_N + 0] = gx; gs[6 * Q_N + 1] = gy; gs[6 * Q_N + 2] = gz; }
+  }
+  STAMP_AT(env, 7);
+  A = s64_args();
+
+  // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)], straight from registers
+  float* row = A->O.obs + ag * Q_D;
+  if (q < 3) {
+    row[9 + 4 * q] = ndx; row[10 + 4 * q] = ndy; row[11 + 4 * q] = ndz; row[12 + 4 * q] = nd;
+  } else {
+    row[0] = px; row[1] = py; row[2] = pz;
+    row[3] = vx; row[4] = vy; row[5] = vz;
+    row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
+  }
+  row[21 + 4 * q] = odx; row[22 + 4 * q] = ody; row[23 + 4 * q] = odz; row[24 + 4 * q] = od;
+  STAMP_AT(env, 8);
+#ifdef SWARM_STAMPS
+  if (lane == 0 && env < (1 << 16)) g_stamps[env * 16 + 12] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // ------------------------------------------------------------------ host side
@@ -2263,6 +2696,13 @@ SWARM_PICK_DECL(2);
 SWARM_PICK_DECL(3);
 // the headline specialisation (SWARM_PART 5)
 __attribute__((visibility("hidden"))) void* swarm_pick_step64(bool persistent, bool physics);
+// the config-2 specialisation (SWARM_PART 6)
+__attribute__((visibility("hidden"))) void* swarm_pick_step16q();
+#if SWARM_HAS_PART(6)
+__attribute__((visibility("hidden"))) void* swarm_pick_step16q() {
+  return reinterpret_cast<void*>(swarm_step16q<Q_WG_ENVS>);
+}
+#endif
 #if SWARM_HAS_PART(5)
 __attribute__((visibility("hidden"))) void* swarm_pick_step64(bool persistent, bool physics) {
   if (physics) return reinterpret_cast<void*>(swarm_step64_phys_once<S64_CH, S64_WG_ENVS>);
@@ -2344,6 +2784,12 @@ int obs_dim_of(const swarm_params_t* p) {
 bool step64_applies(const swarm_params_t* p, const KParams& k) {
   return p->kernel_path == SWARM_PATH_AUTO && k.N == S64_N && k.K == S64_K && k.Ms == S64_MS && k.M >= S64_MS &&
          k.M <= S64_MMAX && (p->dynamics == DYN_KIN || p->dynamics == DYN_PHYS);
+}
+
+// The config-2 specialisation swarm_step16q covers N = 16, K = 3, Ms = 4, 4 <= M <= 16, kinematic.
+bool step16q_applies(const swarm_params_t* p, const KParams& k) {
+  return p->kernel_path == SWARM_PATH_AUTO && k.N == Q_N && k.K == Q_K && k.Ms == Q_MS && k.M >= Q_MS &&
+         k.M <= Q_MMAX && p->dynamics == DYN_KIN;
 }
 
 // Persistent grid of swarm_step64: waves_per_simd x 4 SIMDs x the current device's CUs (E when
@@ -2527,6 +2973,15 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
     if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SWARM_OK;
   }
+  if (mode == MODE_STEP && step16q_applies(p, kp) && !s->env_cfg &&
+      ((uintptr_t)o->terminated | (uintptr_t)o->truncated | (uintptr_t)s->active) % 4 == 0) {
+    const S64Args args{kp, *s, actions, amask, *o};
+    hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step16q()), dim3((kp.E + Q_WG_ENVS - 1) / Q_WG_ENVS),
+                       dim3(64 * Q_WG_ENVS), 0, (hipStream_t)stream, args);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
+    return SWARM_OK;
+  }
   const int lanes = 1 << kp.log2_lanes;
   const int lm = lanes > 64 ? 0 : (lanes == 64 ? 2 : 1);
   const int ks = info.neighbor_slots, msl = info.obstacle_slots;
@@ -2658,6 +3113,15 @@ int swarm_query_launch(const swarm_params_t* p, swarm_launch_info_t* info) {
   KParams kp;
   if (!info) return fail(SWARM_ENULL, "info is NULL");
   const int rc = build_kparams(p, &kp, info);
+  if (rc == SWARM_OK && step16q_applies(p, kp)) {  // one env per 64-lane wave, 4 lanes per drone
+    info->lanes_per_env = 64;
+    info->threads_per_block = 64 * Q_WG_ENVS;
+    info->envs_per_block = Q_WG_ENVS;
+    info->blocks = (kp.E + Q_WG_ENVS - 1) / Q_WG_ENVS;
+    info->lds_bytes = Q_WG_ENVS * (int)sizeof(Q16Lds);
+    info->staged_obs = 0;
+    info->kernel_id = SWARM_KERNEL_STEP16Q;
+  }
   if (rc == SWARM_OK && step64_applies(p, kp)) {  // geometry of the step launch (reset/observe stay generic)
     const int grid = p->dynamics == DYN_PHYS ? kp.E : step64_grid(p, kp.E);
     const int lds_env = (int)sizeof(S64Lds<S64_CH>);
