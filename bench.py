@@ -579,6 +579,8 @@ def main(argv=None):
                                       "16 lanes/clk/SIMD x 1024 SIMDs x 2.4 GHz"}
         metric = METRIC if pol is None else \
             "rollout agent-steps/sec (on-device policy + env step) at N=64 x E=8192 per MI355X"
+        if (n, e) != (64, 8192):  # a config line (--config / --drones / --envs), not the headline
+            metric = metric.split(" at N=")[0] + f" at N={n} x E={e} envs per MI355X (not the headline shape)"
         rec = {
             "metric": metric, "value": value, "unit": "agent-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall_max / args.steps * 1e3,

@@ -2289,6 +2289,40 @@ __device__ __forceinline__ float quad_min(float v) {
   return fminf(v, __uint_as_float(quad_xor2(__float_as_uint(v))));
 }
 
+// Exact (distance, index) keys for the quad-parallel fallback finish: the exact distance's float
+// bits above the index, so one unsigned compare orders by distance, ties by index (the
+// reference's stable order).
+typedef unsigned long long q16_key;
+__device__ __forceinline__ void q16_cx(q16_key& a, q16_key& b) {
+  const q16_key lo = a < b ? a : b;
+  b = a < b ? b : a;
+  a = lo;
+}
+template <int X>
+__device__ __forceinline__ q16_key quad_xor_key(q16_key v) {
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  const uint32_t plo = X == 1 ? quad_xor1(lo) : quad_xor2(lo), phi = X == 1 ? quad_xor1(hi) : quad_xor2(hi);
+  return ((q16_key)phi << 32) | plo;
+}
+// sort this lane's 4 keys, then two bitonic merges with the quad partners (as quad_merge4):
+// every lane of the quad ends with the 4 smallest of the quad's 16 keys, ascending
+__device__ __forceinline__ void q16_quad_select4(q16_key (&k)[4]) {
+  q16_cx(k[0], k[1]); q16_cx(k[2], k[3]); q16_cx(k[0], k[2]); q16_cx(k[1], k[3]); q16_cx(k[1], k[2]);
+#pragma unroll
+  for (int x = 1; x <= 2; ++x) {
+    q16_key c[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const q16_key b = x == 1 ? quad_xor_key<1>(k[3 - i]) : quad_xor_key<2>(k[3 - i]);
+      c[i] = k[i] < b ? k[i] : b;
+    }
+    q16_cx(c[0], c[2]); q16_cx(c[1], c[3]);
+    q16_cx(c[0], c[1]); q16_cx(c[2], c[3]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) k[i] = c[i];
+  }
+}
+
 // One quarter's share of the symmetric pair pass of drone d: rotations q + 1 and q + 5 (r = 8 has
 // no mirror).  PASS 1: d~ keys + formation + running minimum (non-FAST); PASS 0: s' keys only.
 template <int PASS, bool FAST>
@@ -2330,6 +2364,11 @@ __device__ __forceinline__ void q16_pair_pass(const float* __restrict__ soa, int
   }
 }
 
+#ifdef SWARM_STAMPS
+#define Q16_FLAG(f) (q16_flags |= (f))  // slow paths a wave took (tools/stamps16.py)
+#else
+#define Q16_FLAG(f) ((void)0)
+#endif
 template <int G>
 __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(8)))
 swarm_step16q(const S64Args args) {
@@ -2346,6 +2385,7 @@ swarm_step16q(const S64Args args) {
   STAMP_AT(env, 0);
 #ifdef SWARM_STAMPS
   if (lane == 0 && env < (1 << 16)) g_stamps[env * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+  uint32_t q16_flags = 0u;
 #endif
   const int M = A->P.M;
   const size_t ea = (size_t)env * Q_N;
@@ -2442,12 +2482,17 @@ swarm_step16q(const S64Args args) {
   if (fast) {
     const uint32_t keep = A->P.nb_keep;
     pcoll = __uint_as_float(nk[0] | ~keep) * FAST_HI <= A->P.thr_pair;
-    if (!pcoll && __uint_as_float(nk[0] & keep) * FAST_LO <= A->P.thr_pair)
+    if (!pcoll && __uint_as_float(nk[0] & keep) * FAST_LO <= A->P.thr_pair) {
       pcoll = key_zero_hit<true>(nk[0], keep, A->P.s_pair) || exact_pair_collision(L.ring, Q_N, d, px, py, pz, A->P.s_pair);
+      Q16_FLAG(2u);
+    }
   } else {
+    Q16_FLAG(8u);
     pcoll = smin <= A->P.thr_pair * FAST_LO;
-    if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act)
+    if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act) {
       pcoll = exact_pair_collision(L.ring, Q_N, d, px, py, pz, A->P.s_pair);
+      Q16_FLAG(2u);
+    }
   }
   const float curr = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
   float rew = 0.f;
@@ -2500,6 +2545,7 @@ swarm_step16q(const S64Args args) {
   if (do_reset) {
     const long long genv = A->P.env_offset + env;
     episode_new = episode0 + 1u;
+    Q16_FLAG(4u);
     uint32_t wd4[4], wo[4];
     draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)d, wd4);
     draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)(Q_N + (lane < M ? lane : M)), wo);
@@ -2537,15 +2583,15 @@ swarm_step16q(const S64Args args) {
   const uint32_t nim = ~A->P.nb_keep, oim = ~A->P.ob_keep;
   float nd = 0.f, ndx = 0.f, ndy = 0.f, ndz = 0.f, od = 0.f, odx = 0.f, ody = 0.f, odz = 0.f;
   {
-    bool near = false;
+    bool near_nb = false, near_ob = false;
 #pragma unroll
     for (int s = 0; s + 1 < KS; ++s)
-      near = near | (__uint_as_float(nk[s + 1] & A->P.nb_keep) <=
-                     __uint_as_float((nk[s] & A->P.nb_keep) | nim) * FAST_HI);
+      near_nb = near_nb | (__uint_as_float(nk[s + 1] & A->P.nb_keep) <=
+                           __uint_as_float((nk[s] & A->P.nb_keep) | nim) * FAST_HI);
 #pragma unroll
     for (int s = 0; s + 1 < MSL; ++s)
-      near = near | ((ok[s + 1] != KEY_EMPTY) & (__uint_as_float(ok[s + 1] & A->P.ob_keep) <=
-                                                 __uint_as_float((ok[s] & A->P.ob_keep) | oim) * FAST_HI));
+      near_ob = near_ob | ((ok[s + 1] != KEY_EMPTY) & (__uint_as_float(ok[s + 1] & A->P.ob_keep) <=
+                                                       __uint_as_float((ok[s] & A->P.ob_keep) | oim) * FAST_HI));
     // this quarter's slots (q = 3 has no neighbour slot: it repeats slot 2, unused)
     const uint32_t kn = q == 0 ? nk[0] : (q == 1 ? nk[1] : nk[2]);
     const int jn = (d + (int)(kn & nim)) & (Q_N - 1);
@@ -2564,25 +2610,41 @@ swarm_step16q(const S64Args args) {
     const uint32_t last = ok[Q_MS];
     const bool ok_ob = last == KEY_EMPTY || (int)(last & oim) >= M ||
                        __uint_as_float(last & A->P.ob_keep) > (w3 * w3) * FAST_HI;
-    if (__ballot(near || !ok_nb || !ok_ob) != 0) {
-      // rare: the general finish on every lane (near-ties, unproven bounds), quarter q keeps its slots
-      float wd[KS], odv[MSL];
-      int wj[KS], oj[MSL];
-      const bool slow_nb = !finish_keys<KS, false, true>(nk, L.ring, Q_N, d, Q_N - 1, Q_K, A->P.nb_keep, dkey, px, py,
-                                                         pz, wd, wj);
-      const bool slow_ob = !finish_keys<MSL, true, false>(ok, L.obst, M, 0, 0x7fffffff, Q_MS, A->P.ob_keep, false, px,
-                                                          py, pz, odv, oj);
-      if (slow_nb) exact_select<KS, false>(L.ring, Q_N, d, Q_K, max_first(wd, Q_K), px, py, pz, wd, wj);
-      if (slow_ob) exact_select<MSL, true>(L.obst, M, -1, Q_MS, max_first(odv, Q_MS), px, py, pz, odv, oj);
-      const int sn = q < 2 ? q : 2;
-      nd = sn == 0 ? wd[0] : (sn == 1 ? wd[1] : wd[2]);
-      const int jn2 = (sn == 0 ? wj[0] : (sn == 1 ? wj[1] : wj[2])) & (Q_N - 1);
-      const float4 qn2 = L.ring[jn2];
+    // rare (near-ties, unproven bounds): an exact selection split over the quad — quarter q
+    // measures neighbours d + q + 1 + 4i (obstacles q + 4i) exactly, then two DPP merges (what
+    // exact_select does serially, in the reference's (distance, index) order); each side alone
+    if (__ballot(near_nb || !ok_nb) != 0) {
+      q16_key k4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = q + 1 + 4 * i;
+        const int j = (d + r) & (Q_N - 1);
+        const float4 pj = L.ring[j];
+        const float dj = sqrt_rn(sqsum_1d(pj.x - px, pj.y - py, pj.z - pz));
+        k4[i] = r < Q_N ? ((q16_key)__float_as_uint(dj) << 32) | (uint32_t)j : ~0ull;
+      }
+      q16_quad_select4(k4);
+      const q16_key k2 = q == 0 ? k4[0] : (q == 1 ? k4[1] : k4[2]);
+      nd = __uint_as_float((uint32_t)(k2 >> 32));
+      const float4 qn2 = L.ring[(int)k2 & (Q_N - 1)];
       ndx = qn2.x - px; ndy = qn2.y - py; ndz = qn2.z - pz;
-      od = q == 0 ? odv[0] : (q == 1 ? odv[1] : (q == 2 ? odv[2] : odv[3]));
-      const int jo2 = (q == 0 ? oj[0] : (q == 1 ? oj[1] : (q == 2 ? oj[2] : oj[3]))) & (Q_MMAX - 1);
-      const float4 qo2 = L.obst[jo2];
+      Q16_FLAG(1u);
+    }
+    if (__ballot(near_ob || !ok_ob) != 0) {
+      q16_key k4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = q + 4 * i;
+        const float4 om = L.obst[m];
+        const float dm = sqrt_rn(sqsum_f(om.x - px, om.y - py, om.z - pz));
+        k4[i] = m < M ? ((q16_key)__float_as_uint(dm) << 32) | (uint32_t)m : ~0ull;
+      }
+      q16_quad_select4(k4);
+      const q16_key k2 = q == 0 ? k4[0] : (q == 1 ? k4[1] : (q == 2 ? k4[2] : k4[3]));
+      od = __uint_as_float((uint32_t)(k2 >> 32));
+      const float4 qo2 = L.obst[(int)k2 & (Q_MMAX - 1)];
       odx = qo2.x - px; ody = qo2.y - py; odz = qo2.z - pz;
+      Q16_FLAG(16u);
     }
   }
   STAMP_AT(env, 6);
@@ -2645,6 +2707,13 @@ swarm_step16q(const S64Args args) {
   STAMP_AT(env, 8);
 #ifdef SWARM_STAMPS
   if (lane == 0 && env < (1 << 16)) g_stamps[env * 16 + 12] = __builtin_amdgcn_s_memrealtime();
+  {
+    uint32_t fw = 0u;
+#pragma unroll
+    for (uint32_t bit = 1u; bit <= 16u; bit <<= 1)
+      fw |= __ballot((q16_flags & bit) != 0u) != 0 ? bit : 0u;
+    if (lane == 0 && env < (1 << 16)) g_stamps[env * 16 + 13] = fw;
+  }
 #endif
 }
 

@@ -43,7 +43,10 @@ def main(rnd: str) -> None:
                "valu_insts_per_wave": mean["SQ_INSTS_VALU"] / waves,
                "salu_insts_per_wave": mean["SQ_INSTS_SALU"] / waves,
                "lds_insts_per_wave": mean["SQ_INSTS_LDS"] / waves,
-               "lds_bank_conflict_frac": mean["SQ_LDS_BANK_CONFLICT"] / max(mean["SQ_ACTIVE_INST_LDS"], 1),
+               # bank-conflict stall cycles per LDS-instruction issue cycle: two different counters,
+               # so a ratio, not a fraction (it can exceed 1)
+               "lds_bank_conflict_cycles_per_lds_issue_cycle":
+                   mean["SQ_LDS_BANK_CONFLICT"] / max(mean["SQ_ACTIVE_INST_LDS"], 1),
                "waves": waves,
                "correction": "2 x FETCH_SIZE (gfx950 128-B reads tallied at 64 B) + WRITE_SIZE"}
         traffic[key] = rec
