@@ -88,6 +88,9 @@ def parse(argv=None):
                     help="time the whole-job rate with eager launches instead of hipGraph replay")
     ap.add_argument("--ctde", action="store_true", default=None,
                     help="also emit global_state and all-gather it (config 5)")
+    ap.add_argument("--eval", action="store_true",
+                    help="on-device eval metrics every step (EvalTracker: swarm_eval_update per env group "
+                         "after its step; the envs carry infos): the evaluation-protocol rollout")
     ap.add_argument("--policy", choices=("bf16", "f32"), default=None,
                     help="rollout mode: each step = on-device actor inference on the obs tensor "
                          "(swarm_policy_forward, random-init TorchFC 256x256 weights) + the env step")
@@ -290,8 +293,13 @@ def main(argv=None):
     vec = VecSwarm(e, raw, device=dev, auto_reset=True, seed=0, env_offset=offset, dynamics=args.dynamics,
                    with_global_state=args.ctde, persistent=not args.no_persistent,
                    waves_per_simd=args.waves_per_simd, groups=args.groups,
-                   global_state_slots=args.gs_slots if gathering else 1)
+                   global_state_slots=args.gs_slots if gathering else 1, with_infos=args.eval)
     vec.reset()
+    tracker = None
+    if args.eval:
+        from swarm_marl_amd.eval_metrics import EvalTracker
+        tracker = EvalTracker(vec, capacity=1 << 20)  # later episodes past a full segment are dropped
+        tracker.begin()
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     ring = [torch.rand((e, n, 3), device=dev, generator=gen) * 2 - 1 for _ in range(args.ring)]
     pol, pol_act = None, None
@@ -331,6 +339,8 @@ def main(argv=None):
             vec.step_group(g, pol_act)
         else:
             vec.step_group(g, ring[k % args.ring])
+        if tracker is not None:
+            tracker.update_group(g)
         if args.split_reset:
             split_reset(g)
 
@@ -461,7 +471,8 @@ def main(argv=None):
                   if whole is not None else f"hipGraph replay of {args.ring}-step segments") + (
             (f", {G} env groups on {G} HIP streams (" + ("one graph holding all groups" if fused and whole is not None
                                                         else "one graph per group") + ")") if G > 1 else "") + (
-            f" (policy {args.policy} + env step per step)" if pol is not None else "")
+            f" (policy {args.policy} + env step per step)" if pol is not None else "") + (
+            " + eval metrics update per group" if tracker is not None else "")
     else:
         def body():
             t_ev[0].record(stream)
@@ -579,6 +590,8 @@ def main(argv=None):
                                       "16 lanes/clk/SIMD x 1024 SIMDs x 2.4 GHz"}
         metric = METRIC if pol is None else \
             "rollout agent-steps/sec (on-device policy + env step) at N=64 x E=8192 per MI355X"
+        if tracker is not None:
+            metric = metric.replace("agent-steps/sec", "eval-protocol agent-steps/sec (+ on-device eval metrics)", 1)
         if (n, e) != (64, 8192):  # a config line (--config / --drones / --envs), not the headline
             metric = metric.split(" at N=")[0] + f" at N={n} x E={e} envs per MI355X (not the headline shape)"
         rec = {
@@ -622,6 +635,10 @@ def main(argv=None):
                                           "frac": tf / MFMA_PEAK_TFLOPS[args.policy]},
                              "weights": "random-init TorchFC [256, 256] relu (no checkpoint)"}
             rec["roofline"]["note"] = "env-step roofline fields cover the whole rollout step"
+        if tracker is not None:
+            rec["eval"] = {"tracker": "EvalTracker: swarm_eval_update per env group after its step (episode "
+                                      "reward, path length, exact formation error, votes, records)",
+                           "updates": tracker.updates}
         if not args.no_cpu_baseline and world == 1:
             rec["cpu_baseline"] = cpu_baseline_port(n, e, args.cpu_seconds, raw, args.dynamics == "physics")
             if args.cpu_variant_seconds > 0 and not args.no_term and args.dynamics == "kinematic":

@@ -214,23 +214,25 @@ __global__ void __launch_bounds__(EVAL_THREADS * EVAL_WG_ENVS) eval_update_kerne
   if (SWARM_EVAL_ABLATE == 1 || SWARM_EVAL_ABLATE == 4) {
   } else if (n_obs > 1 && a.N == EVAL_THREADS) {
     // one drone per lane: symmetric rotations.  At rotation r lane t measures the pair
-    // (t, t+r) once and hands the distance to lane t+r (ds_bpermute); r = 32 pairs each lane
-    // with its own opposite, measured by both.  Distances are symmetric bit for bit
-    // (|a-b| = |b-a| per component), so each drone sums exactly the reference's terms; only the
-    // f64 summation order differs (np.mean's pairwise order is not reproduced: 1e-9 relative).
+    // (t, t+r); r = 1..31 covers every unordered pair except the 32 opposite ones once, r = 32
+    // covers those twice (lanes t and t+32).  Distances are symmetric bit for bit (|a-b| = |b-a|
+    // per component) and every observed drone divides by the same n_obs - 1, so the reference's
+    // mean over drones of the mean over partners is (2 S_{r<32} + S_{32}) / (n (n - 1)): the same
+    // terms, each measured once; only the f64 summation order differs (np.mean's pairwise order
+    // is not reproduced: 1e-9 relative).
     const float4 p = pos[t];
-    double s_own = 0.0, s_mir = 0.0;  // two chains of dependent f64 adds instead of one
+    double s_a = 0.0, s_b = 0.0;  // two chains of dependent f64 adds instead of one
 #pragma unroll 8
-    for (int r = 1; r <= 32; ++r) {
+    for (int r = 1; r < 32; ++r) {
       const float4 q = pos[(t + r) & (EVAL_THREADS - 1)];
-      float d = norm1d_fast(p.x - q.x, p.y - q.y, p.z - q.z);
-      d = (p.w != 0.f && q.w != 0.f) ? d : -1.f;  // -1: pair not in the observed set
-      const float dm = __shfl(d, (t - r) & (EVAL_THREADS - 1));  // pair (t-r, t), from lane t-r
-      if (d >= 0.f) s_own += fabs((double)d - a.spacing);
-      if (r < 32 && dm >= 0.f) s_mir += fabs((double)dm - a.spacing);
+      const float d = norm1d_fast(p.x - q.x, p.y - q.y, p.z - q.z);
+      const double term = (p.w != 0.f && q.w != 0.f) ? fabs((double)d - a.spacing) : 0.0;
+      if (r & 1) s_a += term; else s_b += term;
     }
-    const double acc = p.w != 0.f ? (s_own + s_mir) / (double)(n_obs - 1) : 0.0;
-    fe = wave_sum(acc) / (double)n_obs;
+    const float4 q = pos[(t + 32) & (EVAL_THREADS - 1)];
+    const float d = norm1d_fast(p.x - q.x, p.y - q.y, p.z - q.z);
+    const double opp = (p.w != 0.f && q.w != 0.f) ? fabs((double)d - a.spacing) : 0.0;
+    fe = wave_sum(2.0 * (s_a + s_b) + opp) / ((double)n_obs * (double)(n_obs - 1));
   } else if (n_obs > 1) {
     double acc = 0.0;
     for (int i = t; i < a.N; i += EVAL_THREADS) {

@@ -111,6 +111,16 @@ class EvalTracker:
                                                  ctypes.byref(self.vec._gout[g]), self._stream()), self.lib,
                       which="eval")
 
+    def update_group(self, g: int) -> None:
+        """Env group g's share of update(), on the current stream and without joining the
+        groups: for callers that step each group on its own stream (bench.py --eval) and call
+        this after the group's step, for every group once per step, group 0 first."""
+        if g == 0:
+            self.updates += 1
+        nat.check(self.lib.swarm_eval_update(ctypes.byref(self.vec._gparams[g]), ctypes.byref(self._group_c(g)),
+                                             ctypes.byref(self.vec._gout[g]), self._stream()), self.lib,
+                  which="eval")
+
     def _group_c(self, g: int) -> nat.SwarmEval:
         self._c.update_index = self.updates
         if self.vec.groups == 1:
