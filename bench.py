@@ -10,9 +10,10 @@ in HBM.  Envs are sharded across ranks with no collective on the step path (weak
 `--envs` envs per GPU, rank r owns the global envs [r*E, (r+1)*E)).
 
 Timing (the driver's contract): W untimed warm-up steps, then exactly K timed steps bracketed by
-a barrier + device synchronize on both sides, the max over ranks.  The K steps are replayed from
+a barrier + device synchronize on both sides, the max over ranks.  K > 256 steps are replayed from
 a hipGraph holding one launch per action tensor of the ring (`value`, `ms_per_step`: the whole-job
-rate without per-step host launch cost); HIP events recorded on the launch stream around that
+rate without per-step host launch cost); short regions (the driver's K = 20) are launched eagerly
+(host launches run ahead of the GPU; a replayed graph's kernels measured slower there); HIP events recorded on the launch stream around that
 timed region give the average launch duration (`roofline.kernel_ms_mean`, the roofline's time
 base; compare `rocprofv3 --kernel-trace --stats` in profiles/).  A second, eager pass with one
 event pair per launch is reported as `ms_per_step_eager` / `kernel_ms_eager_events`.
@@ -103,6 +104,11 @@ def parse(argv=None):
     ap.add_argument("--graph", choices=("split", "fused"), default="split",
                     help="env groups in the timed hipGraph: one graph per group stream, or one graph "
                          "holding every group's chain (fork/join captured)")
+    ap.add_argument("--graph-short", action="store_true",
+                    help="replay hipGraphs for short timed regions too (K <= 256; default there: eager launches)")
+    ap.add_argument("--eager-head", type=int, default=0,
+                    help="short timed regions (K <= 256): launch the first H steps eagerly, then replay a graph "
+                         "of the remaining K - H (the GPU starts while the host launches the graph)")
     ap.add_argument("--warm-graph", choices=("whole", "ring"), default="whole",
                     help="device warm-up replays the timed K-step graph (whole) or the 8-step ring graphs")
     ap.add_argument("--split-reset", action="store_true",
@@ -392,22 +398,25 @@ def main(argv=None):
     # events on the launch stream fork to / join from the group streams, so they bracket the
     # whole batch's K steps.
     t_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-    use_graph = not args.no_graph and gatherer is None
+    # short timed regions (the driver's K = 20) launch eagerly: a replayed graph's kernels ran
+    # slower there (27.5-28.8 vs 30.8-32.3 us per step by events, tools/r03x_cmd.sh); graphs for
+    # long regions, where the host's ~5 us per launch would otherwise matter
+    use_graph = not args.no_graph and gatherer is None and (args.steps > 256 or args.graph_short)
     reps, rem = divmod(args.steps, args.ring)
     if use_graph:
-        def capture(n_steps):  # one graph of n_steps ring steps per group, on its group stream
+        def capture(n_steps, k0=0):  # one graph of n_steps ring steps per group, on its group stream
             out = []
             for g in range(G):
                 gr = torch.cuda.CUDAGraph()
                 # thread_local: the RCCL watchdog thread of a multi-rank run keeps querying its events
                 if G == 1:
                     with torch.cuda.graph(gr, capture_error_mode="thread_local"):
-                        for k in range(n_steps):
+                        for k in range(k0, k0 + n_steps):
                             env_step_group(0, k)
                 else:
                     st = vec.group_streams[g]
                     with torch.cuda.stream(st), torch.cuda.graph(gr, stream=st, capture_error_mode="thread_local"):
-                        for k in range(n_steps):
+                        for k in range(k0, k0 + n_steps):
                             env_step_group(g, k)
                 out.append(gr)
             return out
@@ -434,7 +443,9 @@ def main(argv=None):
         # short timed regions (the driver's K = 20) replay all K steps from one graph per group
         # (or one fused graph), so that the wall clock holds one graph launch per group; longer
         # ones replay ring segments plus a graph of the K % ring remainder
-        whole = ((capture_fused if fused else capture)(args.steps)) if args.steps <= 256 else None
+        head = max(0, min(args.eager_head, args.steps - 1)) if args.steps <= 256 and not fused else 0
+        whole = (capture_fused(args.steps) if fused else capture(args.steps - head, head)) \
+            if args.steps <= 256 else None
         tail = capture(rem) if rem and whole is None else None
 
         def replay_all(gs):
@@ -458,6 +469,8 @@ def main(argv=None):
                 with torch.cuda.stream(vec.group_streams[1]):
                     torch.cuda._sleep(int(args.stagger_us * 2400))
             if whole is not None:
+                for k in range(head):  # eager head: the first kernels start at once
+                    env_step(k)
                 replay_all(whole)
             else:
                 for _ in range(reps):
@@ -467,7 +480,8 @@ def main(argv=None):
             if not (fused and whole is not None):
                 join()
             t_ev[1].record(stream)
-        timing = (f"hipGraph replay of the {args.steps} steps (actions from a {args.ring}-tensor ring)"
+        timing = ((f"{head} eager step(s), then " if head else "") +
+                  f"hipGraph replay of the {args.steps - head} steps (actions from a {args.ring}-tensor ring)"
                   if whole is not None else f"hipGraph replay of {args.ring}-step segments") + (
             (f", {G} env groups on {G} HIP streams (" + ("one graph holding all groups" if fused and whole is not None
                                                         else "one graph per group") + ")") if G > 1 else "") + (
