@@ -54,11 +54,11 @@ MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA peaks, MI355X_MI
 # BASELINE.json configs, per GPU: [2] is the headline (the metric's config), [1] and [4] have
 # their own bench lines (profiles/r02_config_lines.jsonl).
 PRESETS = {
-    "headline": dict(drones=64, envs=8192, ctde=False, groups=2,
+    "headline": dict(drones=64, envs=8192, ctde=False, groups=2, groups_graph=4,
                      label="config 3: N=64 x E=8192 on 1 MI355X (headline); config 4 per GPU"),
     "n16": dict(drones=16, envs=1024, ctde=False,
                 label="config 2: N=16 x E=1024 on 1 MI355X (launch-latency-bound)"),
-    "n256": dict(drones=256, envs=1024, ctde=True, groups=2,
+    "n256": dict(drones=256, envs=1024, ctde=True, groups=2, groups_graph=4,
                  label="config 5 per-GPU slab: N=256 x E=1024 with CTDE global_state"),
 }
 
@@ -100,10 +100,12 @@ def parse(argv=None):
                          "warm-up steps (GPU clocks ramp over ~100 ms; reported in the JSON line)")
     ap.add_argument("--groups", type=int, default=None,
                     help="env groups per GPU, each stepped on its own HIP stream (VecSwarm groups=G); "
-                         "default 2 for the headline and n256, 1 for n16")
+                         "default for the headline and n256: 4 with graph replay (K > 256), else 2; 1 for n16")
     ap.add_argument("--graph", choices=("split", "fused"), default="split",
                     help="env groups in the timed hipGraph: one graph per group stream, or one graph "
                          "holding every group's chain (fork/join captured)")
+    ap.add_argument("--spin-sync", action="store_true",
+                    help="diagnostic: poll the closing event before the closing synchronize")
     ap.add_argument("--graph-short", action="store_true",
                     help="replay hipGraphs for short timed regions too (K <= 256; default there: eager launches)")
     ap.add_argument("--eager-head", type=int, default=0,
@@ -128,7 +130,13 @@ def parse(argv=None):
     a.label = pre["label"]
     a.groups_explicit = a.groups is not None
     if a.groups is None:
-        a.groups = pre.get("groups", 1)
+        # 4 groups where the timed region replays graphs (K > 256, no CTDE gather): 25.2 vs
+        # 26.7 us (headline), 56.2 vs 61.0 us (n256); eager short regions (the driver's K = 20)
+        # keep 2 — four streams' eager launches cost the host ~20 us per step and measured
+        # 44-52 us (profiles/r03_groups_ab.jsonl)
+        gathering = a.ctde and int(os.environ.get("WORLD_SIZE", "1")) > 1
+        graph_long = a.steps > 256 and not a.no_graph and not gathering
+        a.groups = pre.get("groups_graph", pre.get("groups", 1)) if graph_long else pre.get("groups", 1)
     if a.groups < 1:
         ap.error("--groups must be >= 1")
 
@@ -159,14 +167,18 @@ def max_over_ranks(values, world: int, device=None) -> list[float]:
     return [float(x) for x in t.cpu()]
 
 
-def timed_region(body, world: int, sync) -> float:
-    """Barrier + sync, run `body`, sync + barrier; wall seconds of this rank."""
+def timed_region(body, world: int, sync, spin=None) -> float:
+    """Barrier + sync, run `body`, sync + barrier; wall seconds of this rank.  `spin`: an event
+    polled until it completes before the closing sync (diagnostic --spin-sync)."""
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
     sync()
     t0 = time.perf_counter()
     body()
+    if spin is not None:
+        while not spin.query():
+            pass
     sync()
     if world > 1:
         import torch.distributed as dist
@@ -524,7 +536,7 @@ def main(argv=None):
         sync()
         warm_ms = (time.perf_counter() - t0) * 1e3
     gather_t0 = gatherer.k if gatherer is not None else 0
-    wall = timed_region(body, world, sync)
+    wall = timed_region(body, world, sync, spin=t_ev[1] if args.spin_sync else None)
     kern_ms = t_ev[0].elapsed_time(t_ev[1]) / args.steps
 
     # ---- diagnostic pass: eager launches, one event pair around every launch on its stream
