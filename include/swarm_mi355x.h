@@ -65,6 +65,8 @@ extern "C" {
                                    (E > grid; needs state.work, else STEP64 is launched) */
 #define SWARM_KERNEL_STEP16Q 3  /* swarm_step16q: N = 16, K = 3, Ms = 4, 4 <= M <= 16, kinematic step; one
                                    env per 64-lane wave, four lanes per drone (BASELINE config 2) */
+#define SWARM_KERNEL_STEP256 4  /* swarm_step256: N = 256, K = 3, Ms = 4, 4 <= M <= 16, kinematic step; one
+                                   env per 256-thread workgroup, every pair evaluated once (BASELINE config 5) */
 
 /* env_done bits ([E] u8) */
 #define SWARM_ENV_TERMINATED 1u  /* terminated["__all__"] */

@@ -41,7 +41,7 @@
 // Build partitioning: the kernel instantiations are compiled as parallel translation units.
 // SWARM_PART k in 0..3 holds the kernels of (KIND, DYN) = (k >> 1, k & 1); SWARM_PART 4 holds
 // the host side and the C-ABI; SWARM_PART 5 the headline specialisation swarm_step64; SWARM_PART 6
-// the config-2 specialisation swarm_step16q;
+// the config-2 specialisation swarm_step16q; SWARM_PART 7 the config-5 specialisation swarm_step256;
 // SWARM_PART -1 (default) is everything in one unit (tools/).
 #ifndef SWARM_PART
 #define SWARM_PART -1
@@ -2717,6 +2717,535 @@ swarm_step16q(const S64Args args) {
 #endif
 }
 
+// ------------------------------------------------------------------ step256: config 5 (N = 256)
+// Specialisation of the step for one env of exactly 256 drones per 256-thread workgroup (wave w
+// holds drones 64w .. 64w + 63, one per lane), kinematic dynamics + swarm reward, K = 3, Ms = 4,
+// 4 <= M <= 16.  Observations, flags, state and global state equal
+// swarm_kernel<0, 0, 4, 5, 0>'s bit for bit; rewards within the 1e-5 contract (formation partial
+// sums in another order) — tests/test_gpu_step256.py.  The generic block team evaluates every
+// pair twice (once per drone); here every pair is evaluated once and its value reaches the
+// other drone by a lane rotation:
+//  * block (w, w), the wave's own drones: step64's symmetric rotations r = 1 .. 32;
+//  * block (w, w + 1): all 64 rotations; the mirror values belong to the next wave's drones;
+//  * block (w, w + 2): half of it — rotations 0 .. 31 on waves 0 and 1, 1 .. 32 (the other half
+//    seen from the far side) on waves 2 and 3.
+// 128 rotations per wave instead of 255.  Mirror values travel: formation terms and minima as
+// DPP wave rotations (a value added at rotation r has moved r lanes when the pass ends), keys by
+// ds_bpermute; the ones that belong to another wave's drones are handed over through LDS after
+// the pass.  Keys carry a partner code relative to the drone whose list holds them (block delta
+// x 64 + lane offset, a compile-time constant per rotation), decoded to the drone index before
+// the exact finish.  The keys' inserts are as many as before (each drone ranks 255 candidates);
+// distances, square roots and formation terms halve.
+constexpr int H_N = 256;
+constexpr int H_K = 3;
+constexpr int H_MS = 4;
+constexpr int H_MMAX = 16;
+constexpr int H_BL = 128;       // per-block plane segment: 64 drones + their wrap copy
+constexpr int H_PL = 4 * H_BL;  // one coordinate plane over the 4 blocks
+#ifndef SWARM_H_BATCH
+#define SWARM_H_BATCH 8
+#endif
+constexpr int H_BATCH = SWARM_H_BATCH;  // rotations per scheduling batch of the pair passes
+
+struct H256Lds {
+  float px[H_PL], py[H_PL], pz[H_PL], pe[H_PL];  // SoA planes (eligibility in pe)
+  float4 ring[H_N];                              // exact finish, obs rows, exact scans
+  float4 obst[H_MMAX];
+  float osoa[3 * H_MMAX];
+  float4 goal;  // a new episode's goal (drawn by thread M)
+  union {
+    struct {
+      float sum[2][H_N];
+      float mn[2][H_N];
+    } p1;                      // formation sums / minima handed to another wave's drones
+    uint32_t keys[2][4][H_N];  // neighbour key lists handed to another wave's drones
+  } x;
+};
+
+__device__ __forceinline__ void h_put(H256Lds& L, int w, int t, float x, float y, float z, float el) {
+  const int a = H_BL * w + t;
+  L.px[a] = x; L.px[a + 64] = x;
+  L.py[a] = y; L.py[a + 64] = y;
+  L.pz[a] = z; L.pz[a + 64] = z;
+  L.pe[a] = el; L.pe[a + 64] = el;
+  L.ring[64 * w + t] = make_float4(x, y, z, el);
+}
+
+// Formation + minimum pass over rotations RHI, RHI - 1, .., RLO of one block (X/Y/Z/E = the
+// block's plane segments at lane t).  Own side: formation partial sum `esum` (flushed into the
+// f64 `fsum` every 8 rotations) and minimum `mn` of d~ = v_sqrt_f32(s') over eligible pairs.
+// TRAVEL: the pair's value also enters the traveling sum / minimum (the partner's side).
+template <bool FAST, int RHI, int RLO, bool TRAVEL>
+__device__ __forceinline__ void h_seg1(const float* __restrict__ X, const float* __restrict__ Y,
+                                       const float* __restrict__ Z, const float* __restrict__ E, bool self,
+                                       float px, float py, float pz, float ds, double& fsum, float& mn, float& tsum,
+                                       float& tmin) {
+  float esum = 0.f;
+  const float selff = self ? 1.f : 0.f;
+#pragma unroll
+  for (int r = RHI; r >= RLO; r -= 2) {
+    const bool two = r - 1 >= RLO;
+    float d[2];
+    if (two) {
+      const s64_f2 XX = {X[r], X[r - 1]}, YY = {Y[r], Y[r - 1]}, ZZ = {Z[r], Z[r - 1]};
+      const s64_f2 dx = XX - px, dy = YY - py, dz = ZZ - pz;
+      s64_f2 s = dx * dx;
+      s = __builtin_elementwise_fma(dy, dy, s);
+      s = __builtin_elementwise_fma(dz, dz, s);
+      d[0] = __builtin_amdgcn_sqrtf(s.x);
+      d[1] = __builtin_amdgcn_sqrtf(s.y);
+    } else {
+      d[0] = __builtin_amdgcn_sqrtf(sqsum_rank(X[r] - px, Y[r] - py, Z[r] - pz));
+      d[1] = 0.f;
+    }
+    float term[2];
+    if (two) {
+      const s64_f2 V = {d[0], d[1]};
+      const s64_f2 Ed = V - ds;
+      term[0] = fabsf(Ed.x);
+      term[1] = fabsf(Ed.y);
+    } else {
+      term[0] = fabsf(d[0] - ds);
+      term[1] = 0.f;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+      const int rr = r - h;
+      // masked pass: the pair's eligibility as a float factor (partner plane value 0 / 1 times
+      // this drone's), so no per-rotation lane masks stay live; a masked pair's minimum value is
+      // 3e38 (above every threshold) instead of inf
+      float tv = term[h], dv = d[h];
+      if constexpr (!FAST) {
+        const float ef = selff * E[rr];
+        tv = tv * ef;
+        dv = fmaxf(dv, (1.f - ef) * 3e38f);
+      }
+      esum += tv;
+      mn = fminf(mn, dv);
+      if constexpr (TRAVEL) {
+        tsum = wave_ror1(tsum) + tv;
+        tmin = fminf(wave_ror1(tmin), dv);
+      }
+      if (((RHI - rr) & 7) == 7) {
+        fsum += (double)esum;
+        esum = 0.f;
+      }
+    }
+    // batches of H_BATCH rotations: unbounded hoisting of the compile-time-offset LDS reads of a
+    // whole segment costs registers (spills at 4 waves per SIMD)
+    if (((RHI - r) % H_BATCH) == H_BATCH - 2) __builtin_amdgcn_sched_barrier(0);
+  }
+  fsum += (double)esum;
+}
+
+// Keys pass (s' keys) over rotations RHI .. RLO of one block: own keys into `nk` with partner
+// code CO + r; MIRROR: the pair value goes by ds_bpermute to lane t + r, whose target list `mk`
+// takes it with code CM + (64 - r) % 64 (lane offset back to this lane, block delta in CM).
+template <int RHI, int RLO, int CO, int CM, bool MIRROR>
+__device__ __forceinline__ void h_seg0(const float* __restrict__ X, const float* __restrict__ Y,
+                                       const float* __restrict__ Z, uint32_t t4, float px, float py, float pz,
+                                       uint32_t keep, uint32_t (&nk)[4], uint32_t (&mk)[4]) {
+#pragma unroll
+  for (int r = RHI; r >= RLO; r -= 2) {
+    const bool two = r - 1 >= RLO;
+    float s[2];
+    if (two) {
+      const s64_f2 XX = {X[r], X[r - 1]}, YY = {Y[r], Y[r - 1]}, ZZ = {Z[r], Z[r - 1]};
+      const s64_f2 dx = XX - px, dy = YY - py, dz = ZZ - pz;
+      s64_f2 q = dx * dx;
+      q = __builtin_elementwise_fma(dy, dy, q);
+      q = __builtin_elementwise_fma(dz, dz, q);
+      s[0] = q.x;
+      s[1] = q.y;
+    } else {
+      s[0] = sqsum_rank(X[r] - px, Y[r] - py, Z[r] - pz);
+      s[1] = 0.f;
+    }
+    uint32_t rc[2] = {0u, 0u};
+    if constexpr (MIRROR) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !two) break;
+        rc[h] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t4 + (uint32_t)(256 - 4 * (r - h))),
+                                                       (int)__float_as_uint(s[h]));
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+      const int rr = r - h;
+      kins<4>(nk, (__float_as_uint(s[h]) & keep) | (uint32_t)(CO + rr));
+      if constexpr (MIRROR) kins<4>(mk, (rc[h] & keep) | (uint32_t)(CM + ((64 - rr) & 63)));
+    }
+    if (((RHI - r) % H_BATCH) == H_BATCH - 2) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// The 4 smallest of two ascending 4-key lists (bitonic, as quad_merge4)
+__device__ __forceinline__ void h_merge4(uint32_t (&k)[4], const uint32_t (&b)[4]) {
+  uint32_t c[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c[i] = min(k[i], b[3 - i]);
+  const uint32_t c0 = min(c[0], c[2]), c2 = max(c[0], c[2]);
+  const uint32_t c1 = min(c[1], c[3]), c3 = max(c[1], c[3]);
+  k[0] = min(c0, c1); k[1] = max(c0, c1);
+  k[2] = min(c2, c3); k[3] = max(c2, c3);
+}
+
+template <bool FAST>
+__device__ __forceinline__ void h_pass1(H256Lds& L, int w, int t, bool self, float px, float py, float pz, float ds,
+                                        double& fsum, float& smin) {
+  const int b1 = (w + 1) & 3, b2 = (w + 2) & 3;
+  const float* X0 = L.px + H_BL * w + t;  const float* Y0 = L.py + H_BL * w + t;
+  const float* Z0 = L.pz + H_BL * w + t;  const float* E0 = L.pe + H_BL * w + t;
+  const float* X1 = L.px + H_BL * b1 + t; const float* Y1 = L.py + H_BL * b1 + t;
+  const float* Z1 = L.pz + H_BL * b1 + t; const float* E1 = L.pe + H_BL * b1 + t;
+  const float* X2 = L.px + H_BL * b2 + t; const float* Y2 = L.py + H_BL * b2 + t;
+  const float* Z2 = L.pz + H_BL * b2 + t; const float* E2 = L.pe + H_BL * b2 + t;
+  float ta = 0.f, tam = __builtin_inff(), dummy = 0.f, dummym = 0.f;
+  // own block: rotations 31 .. 1 with the traveling mirror, then 32 from both sides
+  h_seg1<FAST, 31, 1, true>(X0, Y0, Z0, E0, self, px, py, pz, ds, fsum, smin, ta, tam);
+  fsum += (double)wave_ror1(ta);
+  smin = fminf(smin, wave_ror1(tam));
+  h_seg1<FAST, 32, 32, false>(X0, Y0, Z0, E0, self, px, py, pz, ds, fsum, smin, dummy, dummym);
+  // block (w, w + 1): rotations 63 .. 0, mirror for wave w + 1's drones
+  float tb = 0.f, tbm = __builtin_inff();
+  h_seg1<FAST, 63, 0, true>(X1, Y1, Z1, E1, self, px, py, pz, ds, fsum, smin, tb, tbm);
+  // block (w, w + 2): half, mirror for wave w + 2's drones
+  float tc = 0.f, tcm = __builtin_inff();
+  if (w < 2) {
+    h_seg1<FAST, 31, 0, true>(X2, Y2, Z2, E2, self, px, py, pz, ds, fsum, smin, tc, tcm);
+  } else {
+    h_seg1<FAST, 32, 1, true>(X2, Y2, Z2, E2, self, px, py, pz, ds, fsum, smin, tc, tcm);
+    tc = wave_ror1(tc);
+    tcm = wave_ror1(tcm);
+  }
+  L.x.p1.sum[0][64 * b1 + t] = tb;
+  L.x.p1.mn[0][64 * b1 + t] = tbm;
+  L.x.p1.sum[1][64 * b2 + t] = tc;
+  L.x.p1.mn[1][64 * b2 + t] = tcm;
+}
+
+__device__ __forceinline__ void h_pass0(H256Lds& L, int w, int t, float px, float py, float pz, uint32_t keep,
+                                        uint32_t (&nk)[4]) {
+  const int b1 = (w + 1) & 3, b2 = (w + 2) & 3;
+  const uint32_t t4 = (uint32_t)t << 2;
+  uint32_t kb[4], kc[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) { kb[s] = KEY_EMPTY; kc[s] = KEY_EMPTY; }
+  // own block: codes r (own) and 64 - r (mirror, same block); rotation 32 from both sides
+  h_seg0<31, 1, 0, 0, true>(L.px + H_BL * w + t, L.py + H_BL * w + t, L.pz + H_BL * w + t, t4, px, py, pz, keep, nk, nk);
+  h_seg0<32, 32, 0, 0, false>(L.px + H_BL * w + t, L.py + H_BL * w + t, L.pz + H_BL * w + t, t4, px, py, pz, keep, nk,
+                              nk);
+  // block (w, w + 1): own code 64 + r (block delta 1); mirror code 192 + (64 - r) % 64 (delta -1)
+  h_seg0<63, 0, 64, 192, true>(L.px + H_BL * b1 + t, L.py + H_BL * b1 + t, L.pz + H_BL * b1 + t, t4, px, py, pz, keep,
+                               nk, kb);
+  // block (w, w + 2): own code 128 + r, mirror code 128 + (64 - r) % 64 (delta +-2)
+  if (w < 2)
+    h_seg0<31, 0, 128, 128, true>(L.px + H_BL * b2 + t, L.py + H_BL * b2 + t, L.pz + H_BL * b2 + t, t4, px, py, pz,
+                                  keep, nk, kc);
+  else
+    h_seg0<32, 1, 128, 128, true>(L.px + H_BL * b2 + t, L.py + H_BL * b2 + t, L.pz + H_BL * b2 + t, t4, px, py, pz,
+                                  keep, nk, kc);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    L.x.keys[0][s][64 * b1 + t] = kb[s];
+    L.x.keys[1][s][64 * b2 + t] = kc[s];
+  }
+}
+
+// partner code -> drone index, for the drone (w, t) whose list holds the key
+__device__ __forceinline__ uint32_t h_decode(uint32_t key, int w, int t, uint32_t keep) {
+  if (key == KEY_EMPTY) return key;
+  const uint32_t c = key & ~keep;
+  const uint32_t j = ((((uint32_t)w + (c >> 6)) & 3u) << 6) | (((uint32_t)t + c) & 63u);
+  return (key & keep) | j;
+}
+
+// step64's straight-line finish (s64_finish_fast) with drone indices in the neighbour keys
+__device__ __forceinline__ bool h_finish_fast(const uint32_t (&nk)[4], const uint32_t (&ok)[5],
+                                              const float4* __restrict__ ring, const float4* __restrict__ obst, int M,
+                                              uint32_t nb_keep, uint32_t ob_keep, float px, float py, float pz,
+                                              float (&wd)[4], int (&wj)[4], float (&od)[5], int (&oj)[5]) {
+  constexpr int K = 3, MS = 4;
+  const uint32_t nim = ~nb_keep, oim = ~ob_keep;
+  bool near = false;
+#pragma unroll
+  for (int s = 0; s + 1 < 4; ++s)
+    near = near | (__uint_as_float(nk[s + 1] & nb_keep) <= __uint_as_float((nk[s] & nb_keep) | nim) * FAST_HI);
+#pragma unroll
+  for (int s = 0; s + 1 < 5; ++s)
+    near = near | ((ok[s + 1] != KEY_EMPTY) &
+                   (__uint_as_float(ok[s + 1] & ob_keep) <= __uint_as_float((ok[s] & ob_keep) | oim) * FAST_HI));
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    const int j = (int)(nk[s] & nim) & (H_N - 1);
+    const float4 q = ring[j];
+    wd[s] = sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
+    wj[s] = j;
+  }
+  wd[K] = __builtin_inff();
+  wj[K] = 0x7fffffff;
+#pragma unroll
+  for (int s = 0; s < MS; ++s) {
+    const int j = (int)(ok[s] & oim);
+    const float4 q = obst[j & (H_MMAX - 1)];
+    od[s] = sqrt_rn(sqsum_f(q.x - px, q.y - py, q.z - pz));
+    oj[s] = j;
+  }
+  od[MS] = __builtin_inff();
+  oj[MS] = 0x7fffffff;
+  // survivor bounds (finish_keys' tails: s' neighbour keys, exact obstacle keys)
+  const float nb_base = __uint_as_float(nk[K] & nb_keep) * FAST_LO;
+  const float wv = wd[K - 1];
+  const bool ok_nb = nb_base > (wv * wv) * FAST_HI;
+  const uint32_t last = ok[MS];
+  const float wo = od[MS - 1];
+  const bool ok_ob = last == KEY_EMPTY || (int)(last & oim) >= M ||
+                     __uint_as_float(last & ob_keep) > (wo * wo) * FAST_HI;
+  return !near && ok_nb && ok_ob;
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) swarm_step256(const S64Args args) {
+  (void)args;  // read through s64_args()
+  constexpr int KS = H_K + 1, MSL = H_MS + 1;
+  __shared__ H256Lds L;
+  const int i = threadIdx.x;  // drone
+  const int w = __builtin_amdgcn_readfirstlane(i >> 6), t = i & 63;
+  S64ArgPtr A = s64_args();
+  const int env = blockIdx.x;
+  if (env >= A->P.E) return;  // whole block
+  const int M = A->P.M;
+  const size_t ag = (size_t)env * H_N + i;
+
+  // ---- loads
+  const float gx0 = A->S.goal[3 * env], gy0 = A->S.goal[3 * env + 1], gz0 = A->S.goal[3 * env + 2];
+  const int stepc = A->S.step_count[env];
+  const uint32_t episode0 = A->S.episode[env];
+  float ax = A->actions[ag * 3], ay = A->actions[ag * 3 + 1], az = A->actions[ag * 3 + 2];
+  float px = A->S.pos[ag * 3], py = A->S.pos[ag * 3 + 1], pz = A->S.pos[ag * 3 + 2];
+  float vx = A->S.vel[ag * 3], vy = A->S.vel[ag * 3 + 1], vz = A->S.vel[ag * 3 + 2];
+  bool act = A->S.active[ag] != 0;
+  const bool has = A->amask == nullptr || A->amask[ag] != 0;
+  if (i < M) {
+    const float* o = A->S.obstacles + ((size_t)env * M + i) * 3;
+    const float ox = o[0], oy = o[1], oz = o[2];
+    L.obst[i] = make_float4(ox, oy, oz, 0.f);
+    L.osoa[i] = ox; L.osoa[H_MMAX + i] = oy; L.osoa[2 * H_MMAX + i] = oz;
+  }
+  float gx = gx0, gy = gy0, gz = gz0;
+  const int n_active = __syncthreads_count(act);
+  A = s64_args();
+
+  // ---- integrate: drone_swarm_env.py:98-117 (swarm_kernel, DYN_KIN)
+  float prev_d = 0.f;
+  if (act) {
+    prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
+    if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
+    ax = clampf(ax, -1.f, 1.f) * A->P.amax;
+    ay = clampf(ay, -1.f, 1.f) * A->P.amax;
+    az = clampf(az, -1.f, 1.f) * A->P.amax;
+    vx = vx + ax * A->P.dt;
+    vy = vy + ay * A->P.dt;
+    vz = vz + az * A->P.dt;
+    const float s_sp = sqsum_1d(vx, vy, vz);
+    if (!(s_sp <= A->P.s_vmax)) {
+      const float sp = sqrt_rn(s_sp);
+      if (!(sp <= A->P.vmax || sp < (float)1e-8)) {
+        vx = (vx / sp) * A->P.vmax;
+        vy = (vy / sp) * A->P.vmax;
+        vz = (vz / sp) * A->P.vmax;
+      }
+    }
+    px = px + vx * A->P.dt;
+    py = py + vy * A->P.dt;
+    pz = pz + vz * A->P.dt;
+  }
+  if (n_active > 0) {
+    px = clampf(px, A->P.neg_half_w, A->P.half_w);
+    py = clampf(py, A->P.neg_half_w, A->P.half_w);
+    pz = clampf(pz, A->P.neg_half_w, A->P.half_w);
+  }
+  h_put(L, w, t, px, py, pz, act ? 1.f : 0.f);
+  const bool fast = __syncthreads_and(act) != 0;  // also the barrier after the puts
+  A = s64_args();
+
+  // ---- formation + minimum pass (every pair once), obstacle pass
+  double fsum = 0.0;
+  float smin = __builtin_inff();
+  if (fast) h_pass1<true>(L, w, t, true, px, py, pz, A->P.ds_f, fsum, smin);
+  else h_pass1<false>(L, w, t, act, px, py, pz, A->P.ds_f, fsum, smin);
+  uint32_t ok[MSL];
+#pragma unroll
+  for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
+  bool ocoll = false;
+  obstacle_pass_s64<MSL, true>(L.osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
+  __syncthreads();  // handed-over sums / minima written
+  fsum += (double)L.x.p1.sum[0][i];
+  fsum += (double)L.x.p1.sum[1][i];
+  smin = fminf(smin, fminf(L.x.p1.mn[0][i], L.x.p1.mn[1][i]));
+  A = s64_args();
+
+  // ---- rewards / terminations: drone_swarm_env.py:120-172 (swarm_kernel, DYN_KIN)
+  bool pcoll = smin <= A->P.thr_pair * FAST_LO;
+  if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act)
+    pcoll = exact_pair_collision(L.ring, H_N, i, px, py, pz, A->P.s_pair);
+  const float curr = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
+  float rew = 0.f;
+  bool reached = false, collided = false, term = false, trunc = false, cont = false;
+  bool term_all = false, trunc_all = false;
+  int new_step = stepc;
+  bool p_coll = false, p_cand = false;
+  if (act) {
+    reached = (double)curr <= A->P.goal_radius;
+    collided = ocoll || pcoll;
+    p_coll = collided;
+    p_cand = !reached && !collided;
+    double r = ((double)prev_d - (double)curr) * A->P.kp;
+    if (n_active > 1) r = r + (-A->P.kf) * (fsum * inv_count(n_active - 1));
+    if (reached) r = r + A->P.r_goal;
+    if (collided) r = r + A->P.r_col;
+    rew = (float)r;
+  }
+  const bool any_c = __syncthreads_or(p_coll) != 0;
+  const bool any_cand = __syncthreads_or(p_cand) != 0;
+  A = s64_args();
+  if (n_active == 0) {
+    term_all = true;
+  } else {
+    new_step = stepc + 1;
+    const bool tl = new_step >= A->P.max_steps;
+    term_all = (!any_cand && !any_c && !tl) || any_c;
+    trunc_all = tl && !term_all;
+    if (act) {
+      const bool done_i = reached || collided;
+      term = done_i;
+      trunc = tl && !done_i;
+      cont = !done_i && !tl && !any_c;
+    }
+  }
+  const bool do_reset = A->P.auto_reset && (term_all || trunc_all);
+  A->O.reward[ag] = rew;
+  A->O.terminated[ag] = term ? 1 : 0;
+  A->O.truncated[ag] = trunc ? 1 : 0;
+  if (A->O.dist_goal) A->O.dist_goal[ag] = curr;
+  if (A->O.info_flags)
+    A->O.info_flags[ag] = (uint8_t)((act ? SWARM_AGENT_STEPPED : 0u) | (act && reached ? SWARM_AGENT_REACHED : 0u) |
+                                    (act && collided ? SWARM_AGENT_COLLISION : 0u) | (cont ? SWARM_AGENT_HAS_OBS : 0u));
+  if (i == 0)
+    A->O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
+                                   (do_reset ? SWARM_ENV_RESET : 0u));
+
+  // ---- in-kernel auto-reset (block-uniform): the new episode, then its keys
+  uint32_t episode_new = episode0;
+  if (do_reset) {
+    episode_new = episode0 + 1u;
+    const long long genv = A->P.env_offset + env;
+    uint32_t wd4[4], wo[4];
+    draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)i, wd4);
+    const bool drawer = i <= M;  // obstacle i (i < M) or the goal (i == M)
+    if (drawer) draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)(H_N + i), wo);
+    const float lo_w = A->P.neg_half_w, wd_w = A->P.width_w;
+    px = uni(wd4[0], lo_w, wd_w);
+    py = uni(wd4[1], lo_w, wd_w);
+    pz = uni(wd4[2], lo_w, wd_w);
+    vx = vy = vz = 0.f;
+    act = true;
+    __syncthreads();  // every read of the old planes / ring / obstacles is done
+    if (drawer) {
+      const float ox = uni(wo[0], lo_w, wd_w), oy = uni(wo[1], lo_w, wd_w), oz = uni(wo[2], lo_w, wd_w);
+      if (i < M) {
+        L.obst[i] = make_float4(ox, oy, oz, 0.f);
+        L.osoa[i] = ox; L.osoa[H_MMAX + i] = oy; L.osoa[2 * H_MMAX + i] = oz;
+      } else {
+        L.goal = make_float4(ox, oy, oz, 0.f);
+      }
+    }
+    h_put(L, w, t, px, py, pz, 1.f);
+    __syncthreads();
+    const float4 g4 = L.goal;
+    gx = g4.x; gy = g4.y; gz = g4.z;
+#pragma unroll
+    for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
+    bool c2 = false;
+    obstacle_pass_s64<MSL, false>(L.osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
+  }
+  A = s64_args();
+  uint32_t nk[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
+  h_pass0(L, w, t, px, py, pz, A->P.nb_keep, nk);
+  __syncthreads();  // handed-over key lists written
+  {
+    uint32_t kb[4], kc[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) { kb[s] = L.x.keys[0][s][i]; kc[s] = L.x.keys[1][s][i]; }
+    h_merge4(nk, kb);
+    h_merge4(nk, kc);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) nk[s] = h_decode(nk[s], w, t, A->P.nb_keep);
+  }
+  A = s64_args();
+
+  // ---- exact top-K of the emitted observation (keys rank by s', drone indices)
+  float wd[KS], od[MSL];
+  int wj[KS], oj[MSL];
+  {
+    const bool okf = h_finish_fast(nk, ok, L.ring, L.obst, M, A->P.nb_keep, A->P.ob_keep, px, py, pz, wd, wj, od, oj);
+    if (__builtin_expect(!okf, 0)) {
+      const bool slow_nb = !finish_keys<KS, false, true>(nk, L.ring, H_N, 0, H_N - 1, H_K, A->P.nb_keep, false, px, py,
+                                                         pz, wd, wj);
+      const bool slow_ob = !finish_keys<MSL, true, false>(ok, L.obst, M, 0, 0x7fffffff, H_MS, A->P.ob_keep, false, px,
+                                                          py, pz, od, oj);
+      if (slow_nb) exact_select<KS, false>(L.ring, H_N, i, H_K, max_first(wd, H_K), px, py, pz, wd, wj);
+      if (slow_ob) exact_select<MSL, true>(L.obst, M, -1, H_MS, max_first(od, H_MS), px, py, pz, od, oj);
+    }
+  }
+  A = s64_args();
+
+  // ---- state write-back
+  const bool new_act = do_reset || cont;
+  A->S.pos[ag * 3] = px; A->S.pos[ag * 3 + 1] = py; A->S.pos[ag * 3 + 2] = pz;
+  A->S.vel[ag * 3] = vx; A->S.vel[ag * 3 + 1] = vy; A->S.vel[ag * 3 + 2] = vz;
+  A->S.active[ag] = new_act ? 1 : 0;
+  if (i == 0) {
+    A->S.step_count[env] = do_reset ? 0 : new_step;
+    if (do_reset) {
+      A->S.episode[env] = episode_new;
+      A->S.goal[3 * env] = gx; A->S.goal[3 * env + 1] = gy; A->S.goal[3 * env + 2] = gz;
+    }
+  }
+  if (do_reset && i < M) {
+    float* o = A->S.obstacles + ((size_t)env * M + i) * 3;
+    const float4 q = L.obst[i];
+    o[0] = q.x; o[1] = q.y; o[2] = q.z;
+  }
+  if (A->O.global_state) {
+    float* gs = A->O.global_state + (size_t)env * (6 * H_N + 3);
+    gs[3 * i] = px; gs[3 * i + 1] = py; gs[3 * i + 2] = pz;
+    gs[3 * H_N + 3 * i] = vx; gs[3 * H_N + 3 * i + 1] = vy; gs[3 * H_N + 3 * i + 2] = vz;
+    if (i == 0) { gs[6 * H_N] = gx; gs[6 * H_N + 1] = gy; gs[6 * H_N + 2] = gz; }
+  }
+  A = s64_args();
+
+  // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)], straight from registers
+  float* row = A->O.obs + ag * (9 + 4 * H_K + 4 * H_MS);
+  row[0] = px; row[1] = py; row[2] = pz;
+  row[3] = vx; row[4] = vy; row[5] = vz;
+  row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
+#pragma unroll
+  for (int s = 0; s < H_K; ++s) {
+    const float4 q = L.ring[wj[s] & (H_N - 1)];
+    row[9 + 4 * s] = q.x - px; row[10 + 4 * s] = q.y - py; row[11 + 4 * s] = q.z - pz; row[12 + 4 * s] = wd[s];
+  }
+#pragma unroll
+  for (int s = 0; s < H_MS; ++s) {
+    const float4 q = L.obst[oj[s] & (H_MMAX - 1)];
+    row[21 + 4 * s] = q.x - px; row[22 + 4 * s] = q.y - py; row[23 + 4 * s] = q.z - pz; row[24 + 4 * s] = od[s];
+  }
+}
+
 // ------------------------------------------------------------------ host side
 typedef void (*step64_fn)(const S64Args);
 typedef void (*kernel_fn)(const KParams, const swarm_state_t, const float*, const uint8_t*, const swarm_out_t,
@@ -2767,6 +3296,11 @@ SWARM_PICK_DECL(3);
 __attribute__((visibility("hidden"))) void* swarm_pick_step64(bool persistent, bool physics);
 // the config-2 specialisation (SWARM_PART 6)
 __attribute__((visibility("hidden"))) void* swarm_pick_step16q();
+// the config-5 specialisation (SWARM_PART 7)
+__attribute__((visibility("hidden"))) void* swarm_pick_step256();
+#if SWARM_HAS_PART(7)
+__attribute__((visibility("hidden"))) void* swarm_pick_step256() { return reinterpret_cast<void*>(swarm_step256); }
+#endif
 #if SWARM_HAS_PART(6)
 __attribute__((visibility("hidden"))) void* swarm_pick_step16q() {
   return reinterpret_cast<void*>(swarm_step16q<Q_WG_ENVS>);
@@ -2859,6 +3393,12 @@ bool step64_applies(const swarm_params_t* p, const KParams& k) {
 bool step16q_applies(const swarm_params_t* p, const KParams& k) {
   return p->kernel_path == SWARM_PATH_AUTO && k.N == Q_N && k.K == Q_K && k.Ms == Q_MS && k.M >= Q_MS &&
          k.M <= Q_MMAX && p->dynamics == DYN_KIN;
+}
+
+// The config-5 specialisation swarm_step256 covers N = 256, K = 3, Ms = 4, 4 <= M <= 16, kinematic.
+bool step256_applies(const swarm_params_t* p, const KParams& k) {
+  return p->kernel_path == SWARM_PATH_AUTO && k.N == H_N && k.K == H_K && k.Ms == H_MS && k.M >= H_MS &&
+         k.M <= H_MMAX && p->dynamics == DYN_KIN;
 }
 
 // Persistent grid of swarm_step64: waves_per_simd x 4 SIMDs x the current device's CUs (E when
@@ -3051,6 +3591,14 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
     if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SWARM_OK;
   }
+  if (mode == MODE_STEP && step256_applies(p, kp) && !s->env_cfg) {
+    const S64Args args{kp, *s, actions, amask, *o};
+    hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step256()), dim3(kp.E), dim3(H_N), 0,
+                       (hipStream_t)stream, args);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
+    return SWARM_OK;
+  }
   const int lanes = 1 << kp.log2_lanes;
   const int lm = lanes > 64 ? 0 : (lanes == 64 ? 2 : 1);
   const int ks = info.neighbor_slots, msl = info.obstacle_slots;
@@ -3190,6 +3738,15 @@ int swarm_query_launch(const swarm_params_t* p, swarm_launch_info_t* info) {
     info->lds_bytes = Q_WG_ENVS * (int)sizeof(Q16Lds);
     info->staged_obs = 0;
     info->kernel_id = SWARM_KERNEL_STEP16Q;
+  }
+  if (rc == SWARM_OK && step256_applies(p, kp)) {  // one env per 256-thread workgroup, one lane per drone
+    info->lanes_per_env = H_N;
+    info->threads_per_block = H_N;
+    info->envs_per_block = 1;
+    info->blocks = kp.E;
+    info->lds_bytes = (int)sizeof(H256Lds);
+    info->staged_obs = 0;
+    info->kernel_id = SWARM_KERNEL_STEP256;
   }
   if (rc == SWARM_OK && step64_applies(p, kp)) {  // geometry of the step launch (reset/observe stay generic)
     const int grid = p->dynamics == DYN_PHYS ? kp.E : step64_grid(p, kp.E);

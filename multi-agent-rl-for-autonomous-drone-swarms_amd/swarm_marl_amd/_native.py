@@ -23,6 +23,7 @@ KERNEL_GENERIC = 0
 KERNEL_STEP64 = 1
 KERNEL_STEP64_PERSISTENT = 2
 KERNEL_STEP16Q = 3
+KERNEL_STEP256 = 4
 
 SWARM_OK = 0
 SWARM_EINVAL = -1

@@ -89,6 +89,11 @@ def test_launch_geometry(nat, lib, n):
         assert info.threads_per_block == 256 and info.envs_per_block == 4
         assert info.blocks == 250 and 0 < info.lds_bytes <= 160 * 1024
         return
+    if info.kernel_id == nat.KERNEL_STEP256:  # config-5 specialisation: one env per 256-thread workgroup
+        assert n == 256 and info.lanes_per_env == 256 and info.staged_obs == 0
+        assert info.threads_per_block == 256 and info.envs_per_block == 1
+        assert info.blocks == 1000 and 0 < info.lds_bytes <= 64 * 1024
+        return
     assert info.lanes_per_env == lanes
     if info.kernel_id == nat.KERNEL_STEP64:  # headline specialisation: 4 one-env waves per workgroup
         assert info.threads_per_block == 256 and info.envs_per_block == 4
@@ -106,12 +111,13 @@ def test_launch_geometry(nat, lib, n):
 
 def test_obs_direct_threshold(nat, lib):
     info = nat.SwarmLaunchInfo()
-    # (N = 16 with the default K / Ms / M runs swarm_step16q, rows from registers at any E: the
-    # generic kernel's threshold is checked at N = 16 with K = 4)
+    # (N = 16 / 256 with the default K / Ms / M run swarm_step16q / swarm_step256, rows from
+    # registers at any E: the generic kernel's threshold is checked there with K = 4)
     for n, e, staged, extra in [(16, 1024, 0, {}), (16, 32768, 0, {}), (16, 1024, 0, {"neighbor_k": 4}),
                                 (16, 8192, 0, {"neighbor_k": 4}), (16, 8193, 1, {"neighbor_k": 4}),
-                                (16, 32768, 1, {"neighbor_k": 4}), (256, 1024, 0, {}),
-                                (256, 4096, 1, {}), (64, 1024, 1, {}), (3, 4, 0, {})]:
+                                (16, 32768, 1, {"neighbor_k": 4}), (256, 1024, 0, {"neighbor_k": 4}),
+                                (256, 4096, 1, {"neighbor_k": 4}), (256, 4096, 0, {}), (64, 1024, 1, {}),
+                                (3, 4, 0, {})]:
         p = _params(nat, lib, num_drones=n, num_envs=e, **extra)
         assert lib.swarm_query_launch(ctypes.byref(p), ctypes.byref(info)) == 0
         assert info.staged_obs == staged, (n, e)
