@@ -35,7 +35,8 @@ def main(rnd: str) -> None:
             mean[c] = sum(vv) / len(vv)
         hbm = (2 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024
         waves = mean["SQ_WAVES"]
-        rec = {"kernel": name.replace("void (anonymous namespace)::", "").split("((")[0].split("(")[0],
+        short = name.replace("void ", "").replace("(anonymous namespace)::", "")
+        rec = {"kernel": short.split("(")[0],
                "round": rnd, "hbm_bytes_per_launch": hbm,
                "fetch_size_kb": mean["FETCH_SIZE"], "write_size_kb": mean["WRITE_SIZE"],
                "algorithmic_bytes_per_launch": ALG[cfg],

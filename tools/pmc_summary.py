@@ -12,7 +12,7 @@ def load(root):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = row["Kernel_Name"]
-                if "swarm_kernel" not in k and "swarm_step64" not in k and "policy_mlp" not in k:
+                if not any(s in k for s in ("swarm_kernel", "swarm_step64", "swarm_step16q", "swarm_step256", "policy_mlp")):
                     continue
                 acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return acc
