@@ -2741,14 +2741,16 @@ constexpr int H_K = 3;
 constexpr int H_MS = 4;
 constexpr int H_MMAX = 16;
 constexpr int H_BL = 128;       // per-block plane segment: 64 drones + their wrap copy
-constexpr int H_PL = 4 * H_BL;  // one coordinate plane over the 4 blocks
 #ifndef SWARM_H_BATCH
 #define SWARM_H_BATCH 8
 #endif
 constexpr int H_BATCH = SWARM_H_BATCH;  // rotations per scheduling batch of the pair passes
 
 struct H256Lds {
-  float px[H_PL], py[H_PL], pz[H_PL], pe[H_PL];  // SoA planes (eligibility in pe)
+  // SoA planes per block: seg[b][plane][u], planes x, y, z, eligibility; drone 64b + u at u and
+  // u + 64.  Lane t of a pass reads block b's rotation r at base + r with two bases (x / y and
+  // z / eligibility), every plane within ds_read2_b32's 255-dword offset reach
+  float seg[4][4][H_BL];
   float4 ring[H_N];                              // exact finish, obs rows, exact scans
   float4 obst[H_MMAX];
   float osoa[3 * H_MMAX];
@@ -2763,12 +2765,27 @@ struct H256Lds {
 };
 
 __device__ __forceinline__ void h_put(H256Lds& L, int w, int t, float x, float y, float z, float el) {
-  const int a = H_BL * w + t;
-  L.px[a] = x; L.px[a + 64] = x;
-  L.py[a] = y; L.py[a + 64] = y;
-  L.pz[a] = z; L.pz[a + 64] = z;
-  L.pe[a] = el; L.pe[a + 64] = el;
+  L.seg[w][0][t] = x; L.seg[w][0][t + 64] = x;
+  L.seg[w][1][t] = y; L.seg[w][1][t + 64] = y;
+  L.seg[w][2][t] = z; L.seg[w][2][t + 64] = z;
+  L.seg[w][3][t] = el; L.seg[w][3][t + 64] = el;
   L.ring[64 * w + t] = make_float4(x, y, z, el);
+}
+
+// Lane t's two read bases into block b's planes (x / y and z / eligibility) as opaque LDS
+// addresses, so every rotation's read is an immediate offset of ds_read2_b32
+__device__ __forceinline__ void h_bases(H256Lds& L, int b, int t, s64_lds_cf*& P0, s64_lds_cf*& P1) {
+  P0 = (s64_lds_cf*)&L.seg[b][0][t];
+  P1 = (s64_lds_cf*)&L.seg[b][2][t];
+  asm volatile("" : "+v"(P0), "+v"(P1));
+}
+// Traveling minima are kept as float bits and reduced with v_min_u32 (every value is a
+// non-negative float, whose bit patterns order like the floats): an integer min takes the
+// rotated operand without the canonicalising v_max that v_min_f32 needs, so the DPP move folds
+// into v_min_u32's DPP form (a full-wave rotation gives every lane a source: bound_ctrl changes
+// nothing here)
+__device__ __forceinline__ uint32_t wave_ror1_u(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x13C, 0xF, 0xF, true);
 }
 
 // Formation + minimum pass over rotations RHI, RHI - 1, .., RLO of one block (X/Y/Z/E = the
@@ -2776,10 +2793,13 @@ __device__ __forceinline__ void h_put(H256Lds& L, int w, int t, float x, float y
 // f64 `fsum` every 8 rotations) and minimum `mn` of d~ = v_sqrt_f32(s') over eligible pairs.
 // TRAVEL: the pair's value also enters the traveling sum / minimum (the partner's side).
 template <bool FAST, int RHI, int RLO, bool TRAVEL>
-__device__ __forceinline__ void h_seg1(const float* __restrict__ X, const float* __restrict__ Y,
-                                       const float* __restrict__ Z, const float* __restrict__ E, bool self,
+__device__ __forceinline__ void h_seg1(s64_lds_cf* __restrict__ P0, s64_lds_cf* __restrict__ P1, bool self,
                                        float px, float py, float pz, float ds, double& fsum, float& mn, float& tsum,
-                                       float& tmin) {
+                                       uint32_t& tmin) {
+  s64_lds_cf* X = P0;
+  s64_lds_cf* Y = P0 + H_BL;
+  s64_lds_cf* Z = P1;
+  s64_lds_cf* E = P1 + H_BL;
   float esum = 0.f;
   const float selff = self ? 1.f : 0.f;
 #pragma unroll
@@ -2825,7 +2845,7 @@ __device__ __forceinline__ void h_seg1(const float* __restrict__ X, const float*
       mn = fminf(mn, dv);
       if constexpr (TRAVEL) {
         tsum = wave_ror1(tsum) + tv;
-        tmin = fminf(wave_ror1(tmin), dv);
+        tmin = min(wave_ror1_u(tmin), __float_as_uint(dv));
       }
       if (((RHI - rr) & 7) == 7) {
         fsum += (double)esum;
@@ -2843,9 +2863,15 @@ __device__ __forceinline__ void h_seg1(const float* __restrict__ X, const float*
 // code CO + r; MIRROR: the pair value goes by ds_bpermute to lane t + r, whose target list `mk`
 // takes it with code CM + (64 - r) % 64 (lane offset back to this lane, block delta in CM).
 template <int RHI, int RLO, int CO, int CM, bool MIRROR>
-__device__ __forceinline__ void h_seg0(const float* __restrict__ X, const float* __restrict__ Y,
-                                       const float* __restrict__ Z, uint32_t t4, float px, float py, float pz,
-                                       uint32_t keep, uint32_t (&nk)[4], uint32_t (&mk)[4]) {
+__device__ __forceinline__ void h_seg0(s64_lds_cf* __restrict__ P0, s64_lds_cf* __restrict__ P1, uint32_t t4, float px,
+                                       float py, float pz, uint32_t keep, uint32_t (&nk)[4], uint32_t (&mk)[4]) {
+  s64_lds_cf* X = P0;
+  s64_lds_cf* Y = P0 + H_BL;
+  s64_lds_cf* Z = P1;
+  // keep in a VGPR: (value & keep) | code is then one v_and_or_b32 with the code from an SGPR
+  // (a VOP3 literal is not encodable on gfx9)
+  uint32_t keepv = keep;
+  asm volatile("" : "+v"(keepv));
 #pragma unroll
   for (int r = RHI; r >= RLO; r -= 2) {
     const bool two = r - 1 >= RLO;
@@ -2875,8 +2901,8 @@ __device__ __forceinline__ void h_seg0(const float* __restrict__ X, const float*
     for (int h = 0; h < 2; ++h) {
       if (h == 1 && !two) break;
       const int rr = r - h;
-      kins<4>(nk, (__float_as_uint(s[h]) & keep) | (uint32_t)(CO + rr));
-      if constexpr (MIRROR) kins<4>(mk, (rc[h] & keep) | (uint32_t)(CM + ((64 - rr) & 63)));
+      kins<4>(nk, (__float_as_uint(s[h]) & keepv) | (uint32_t)(CO + rr));
+      if constexpr (MIRROR) kins<4>(mk, (rc[h] & keepv) | (uint32_t)(CM + ((64 - rr) & 63)));
     }
     if (((RHI - r) % H_BATCH) == H_BATCH - 2) __builtin_amdgcn_sched_barrier(0);
   }
@@ -2897,34 +2923,35 @@ template <bool FAST>
 __device__ __forceinline__ void h_pass1(H256Lds& L, int w, int t, bool self, float px, float py, float pz, float ds,
                                         double& fsum, float& smin) {
   const int b1 = (w + 1) & 3, b2 = (w + 2) & 3;
-  const float* X0 = L.px + H_BL * w + t;  const float* Y0 = L.py + H_BL * w + t;
-  const float* Z0 = L.pz + H_BL * w + t;  const float* E0 = L.pe + H_BL * w + t;
-  const float* X1 = L.px + H_BL * b1 + t; const float* Y1 = L.py + H_BL * b1 + t;
-  const float* Z1 = L.pz + H_BL * b1 + t; const float* E1 = L.pe + H_BL * b1 + t;
-  const float* X2 = L.px + H_BL * b2 + t; const float* Y2 = L.py + H_BL * b2 + t;
-  const float* Z2 = L.pz + H_BL * b2 + t; const float* E2 = L.pe + H_BL * b2 + t;
-  float ta = 0.f, tam = __builtin_inff(), dummy = 0.f, dummym = 0.f;
+  s64_lds_cf *A0, *A1, *B0, *B1, *C0, *C1;
+  h_bases(L, w, t, A0, A1);
+  h_bases(L, b1, t, B0, B1);
+  h_bases(L, b2, t, C0, C1);
+  float ta = 0.f, dummy = 0.f;
+  uint32_t tam = 0x7f800000u, dummym = 0x7f800000u;
   // own block: rotations 31 .. 1 with the traveling mirror, then 32 from both sides
-  h_seg1<FAST, 31, 1, true>(X0, Y0, Z0, E0, self, px, py, pz, ds, fsum, smin, ta, tam);
+  h_seg1<FAST, 31, 1, true>(A0, A1, self, px, py, pz, ds, fsum, smin, ta, tam);
   fsum += (double)wave_ror1(ta);
-  smin = fminf(smin, wave_ror1(tam));
-  h_seg1<FAST, 32, 32, false>(X0, Y0, Z0, E0, self, px, py, pz, ds, fsum, smin, dummy, dummym);
+  smin = fminf(smin, __uint_as_float(wave_ror1_u(tam)));
+  h_seg1<FAST, 32, 32, false>(A0, A1, self, px, py, pz, ds, fsum, smin, dummy, dummym);
   // block (w, w + 1): rotations 63 .. 0, mirror for wave w + 1's drones
-  float tb = 0.f, tbm = __builtin_inff();
-  h_seg1<FAST, 63, 0, true>(X1, Y1, Z1, E1, self, px, py, pz, ds, fsum, smin, tb, tbm);
+  float tb = 0.f;
+  uint32_t tbm = 0x7f800000u;
+  h_seg1<FAST, 63, 0, true>(B0, B1, self, px, py, pz, ds, fsum, smin, tb, tbm);
   // block (w, w + 2): half, mirror for wave w + 2's drones
-  float tc = 0.f, tcm = __builtin_inff();
+  float tc = 0.f;
+  uint32_t tcm = 0x7f800000u;
   if (w < 2) {
-    h_seg1<FAST, 31, 0, true>(X2, Y2, Z2, E2, self, px, py, pz, ds, fsum, smin, tc, tcm);
+    h_seg1<FAST, 31, 0, true>(C0, C1, self, px, py, pz, ds, fsum, smin, tc, tcm);
   } else {
-    h_seg1<FAST, 32, 1, true>(X2, Y2, Z2, E2, self, px, py, pz, ds, fsum, smin, tc, tcm);
+    h_seg1<FAST, 32, 1, true>(C0, C1, self, px, py, pz, ds, fsum, smin, tc, tcm);
     tc = wave_ror1(tc);
-    tcm = wave_ror1(tcm);
+    tcm = wave_ror1_u(tcm);
   }
   L.x.p1.sum[0][64 * b1 + t] = tb;
-  L.x.p1.mn[0][64 * b1 + t] = tbm;
+  L.x.p1.mn[0][64 * b1 + t] = __uint_as_float(tbm);
   L.x.p1.sum[1][64 * b2 + t] = tc;
-  L.x.p1.mn[1][64 * b2 + t] = tcm;
+  L.x.p1.mn[1][64 * b2 + t] = __uint_as_float(tcm);
 }
 
 __device__ __forceinline__ void h_pass0(H256Lds& L, int w, int t, float px, float py, float pz, uint32_t keep,
@@ -2935,19 +2962,19 @@ __device__ __forceinline__ void h_pass0(H256Lds& L, int w, int t, float px, floa
 #pragma unroll
   for (int s = 0; s < 4; ++s) { kb[s] = KEY_EMPTY; kc[s] = KEY_EMPTY; }
   // own block: codes r (own) and 64 - r (mirror, same block); rotation 32 from both sides
-  h_seg0<31, 1, 0, 0, true>(L.px + H_BL * w + t, L.py + H_BL * w + t, L.pz + H_BL * w + t, t4, px, py, pz, keep, nk, nk);
-  h_seg0<32, 32, 0, 0, false>(L.px + H_BL * w + t, L.py + H_BL * w + t, L.pz + H_BL * w + t, t4, px, py, pz, keep, nk,
-                              nk);
+  s64_lds_cf *A0, *A1, *B0, *B1, *C0, *C1;
+  h_bases(L, w, t, A0, A1);
+  h_bases(L, b1, t, B0, B1);
+  h_bases(L, b2, t, C0, C1);
+  h_seg0<31, 1, 0, 0, true>(A0, A1, t4, px, py, pz, keep, nk, nk);
+  h_seg0<32, 32, 0, 0, false>(A0, A1, t4, px, py, pz, keep, nk, nk);
   // block (w, w + 1): own code 64 + r (block delta 1); mirror code 192 + (64 - r) % 64 (delta -1)
-  h_seg0<63, 0, 64, 192, true>(L.px + H_BL * b1 + t, L.py + H_BL * b1 + t, L.pz + H_BL * b1 + t, t4, px, py, pz, keep,
-                               nk, kb);
+  h_seg0<63, 0, 64, 192, true>(B0, B1, t4, px, py, pz, keep, nk, kb);
   // block (w, w + 2): own code 128 + r, mirror code 128 + (64 - r) % 64 (delta +-2)
   if (w < 2)
-    h_seg0<31, 0, 128, 128, true>(L.px + H_BL * b2 + t, L.py + H_BL * b2 + t, L.pz + H_BL * b2 + t, t4, px, py, pz,
-                                  keep, nk, kc);
+    h_seg0<31, 0, 128, 128, true>(C0, C1, t4, px, py, pz, keep, nk, kc);
   else
-    h_seg0<32, 1, 128, 128, true>(L.px + H_BL * b2 + t, L.py + H_BL * b2 + t, L.pz + H_BL * b2 + t, t4, px, py, pz,
-                                  keep, nk, kc);
+    h_seg0<32, 1, 128, 128, true>(C0, C1, t4, px, py, pz, keep, nk, kc);
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     L.x.keys[0][s][64 * b1 + t] = kb[s];
