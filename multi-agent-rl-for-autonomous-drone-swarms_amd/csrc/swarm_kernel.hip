@@ -3034,6 +3034,7 @@ __device__ __forceinline__ bool h_finish_fast(const uint32_t (&nk)[4], const uin
   return !near && ok_nb && ok_ob;
 }
 
+#if SWARM_HAS_PART(7)  // emitted in its own translation unit only
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) swarm_step256(const S64Args args) {
   (void)args;  // read through s64_args()
   constexpr int KS = H_K + 1, MSL = H_MS + 1;
@@ -3272,6 +3273,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     row[21 + 4 * s] = q.x - px; row[22 + 4 * s] = q.y - py; row[23 + 4 * s] = q.z - pz; row[24 + 4 * s] = od[s];
   }
 }
+#endif
 
 // ------------------------------------------------------------------ host side
 typedef void (*step64_fn)(const S64Args);

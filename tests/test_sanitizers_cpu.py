@@ -133,7 +133,7 @@ def test_cabi_host_asan_ubsan(tmp_path):
     if rt is None:
         pytest.skip("clang ASan runtime not found under /opt/rocm/lib/llvm")
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
-    kernels = [OBJ / f"swarm_kernel.part{k}.o" for k in (0, 1, 2, 3, 5, 6)]
+    kernels = [OBJ / f"swarm_kernel.part{k}.o" for k in (0, 1, 2, 3, 5, 6, 7)]
     if not all(k.exists() for k in kernels):
         pytest.skip("product kernel objects missing (run __graft_entry__.build() first)")
     san = ["-Xarch_host", "-fsanitize=address,undefined", "-Xarch_host", "-fno-omit-frame-pointer",
