@@ -2755,6 +2755,7 @@ struct H256Lds {
   float4 obst[H_MMAX];
   float osoa[3 * H_MMAX];
   float4 goal;  // a new episode's goal (drawn by thread M)
+  uint32_t red[4];  // per-wave vote bits of the reward phase
   union {
     struct {
       float sum[2][H_N];
@@ -3136,8 +3137,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     if (collided) r = r + A->P.r_col;
     rew = (float)r;
   }
-  const bool any_c = __syncthreads_or(p_coll) != 0;
-  const bool any_cand = __syncthreads_or(p_cand) != 0;
+  // both block votes through one barrier: wave ballots -> one word per wave
+  {
+    const bool wc = __ballot(p_coll) != 0, wd = __ballot(p_cand) != 0;
+    if (t == 0) L.red[w] = (wc ? 1u : 0u) | (wd ? 2u : 0u);
+  }
+  __syncthreads();
+  const uint32_t votes = L.red[0] | L.red[1] | L.red[2] | L.red[3];
+  const bool any_c = (votes & 1u) != 0, any_cand = (votes & 2u) != 0;
   A = s64_args();
   if (n_active == 0) {
     term_all = true;
