@@ -1,0 +1,8 @@
+bash tools/gpu_r03.sh r03ak \
+ "suite:900:python -u -m pytest tests -m gpu -q --maxfail 5 --timeout 120 --timeout-method thread" \
+ "smoke:300:python -c 'import __graft_entry__ as g; g.smoke()'" \
+ "def:200:python bench.py" \
+ "drv:120:python bench.py --gpus 1 --steps 20 --warmup 5" \
+ "drv2:120:python bench.py --gpus 1 --steps 20 --warmup 5" \
+ "n256:200:python bench.py --config n256" \
+ "n16:200:python bench.py --config n16"
