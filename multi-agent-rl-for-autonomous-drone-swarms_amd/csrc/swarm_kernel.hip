@@ -2546,24 +2546,27 @@ swarm_step16q(const S64Args args) {
     const long long genv = A->P.env_offset + env;
     episode_new = episode0 + 1u;
     Q16_FLAG(4u);
-    uint32_t wd4[4], wo[4];
-    draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)d, wd4);
-    draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)(Q_N + (lane < M ? lane : M)), wo);
+    // one Philox block per lane: quarters 0 / 1 drone d, quarter 2 obstacle d (d < M), quarter 3
+    // the goal (block N + M) — the blocks of swarm_kernel's draw_env, one round of the generator
+    // instead of two per lane
+    const uint32_t blk = q < 2 ? (uint32_t)d : (q == 2 ? (uint32_t)(Q_N + d) : (uint32_t)(Q_N + M));
+    uint32_t wv[4];
+    draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, blk, wv);
     const float lo_w = A->P.neg_half_w, wd_w = A->P.width_w;
-    px = uni(wd4[0], lo_w, wd_w);
-    py = uni(wd4[1], lo_w, wd_w);
-    pz = uni(wd4[2], lo_w, wd_w);
+    const float ux = uni(wv[0], lo_w, wd_w), uy = uni(wv[1], lo_w, wd_w), uz = uni(wv[2], lo_w, wd_w);
+    px = quad_bcast<0>(ux);
+    py = quad_bcast<0>(uy);
+    pz = quad_bcast<0>(uz);
     vx = vy = vz = 0.f;
     act = true;
-    const float ox = uni(wo[0], lo_w, wd_w), oy = uni(wo[1], lo_w, wd_w), oz = uni(wo[2], lo_w, wd_w);
     wave_sync();  // every read of the old ring / obstacles is done
-    if (lane < M) {
-      L.obst[lane] = make_float4(ox, oy, oz, 0.f);
-      L.osoa[lane] = ox; L.osoa[Q_MMAX + lane] = oy; L.osoa[2 * Q_MMAX + lane] = oz;
+    if (q == 2 && d < M) {
+      L.obst[d] = make_float4(ux, uy, uz, 0.f);
+      L.osoa[d] = ux; L.osoa[Q_MMAX + d] = uy; L.osoa[2 * Q_MMAX + d] = uz;
     }
-    gx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ox), M));
-    gy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(oy), M));
-    gz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(oz), M));
+    gx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ux), 3));
+    gy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(uy), 3));
+    gz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(uz), 3));
     put(1.f);
     wave_sync();
 #pragma unroll
