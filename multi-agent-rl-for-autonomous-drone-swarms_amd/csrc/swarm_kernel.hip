@@ -2369,6 +2369,17 @@ __device__ __forceinline__ void q16_pair_pass(const float* __restrict__ soa, int
 #else
 #define Q16_FLAG(f) ((void)0)
 #endif
+// The latency-bound specialisations (step16q, step256: one or four waves per SIMD) read the
+// kernarg segment through one pointer, so the compiler batches the parameter loads at the top
+// instead of a dependent scalar round trip at each phase (step64's per-phase re-fetch keeps the
+// persistent loop's SGPRs free; SWARM_LAT_REFETCH=1 restores it here, diagnostics only).
+#ifndef SWARM_LAT_REFETCH_ON
+#define SWARM_LAT_REFETCH_ON 0
+#endif
+#define SWARM_LAT_REFETCH(A) \
+  do {                       \
+    if (SWARM_LAT_REFETCH_ON) (A) = s64_args(); \
+  } while (0)
 template <int G>
 __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(8)))
 swarm_step16q(const S64Args args) {
@@ -2416,7 +2427,7 @@ swarm_step16q(const S64Args args) {
   const uint32_t episode0 = (uint32_t)__builtin_amdgcn_readlane(gse, 4);
   const int n_active = __popcll(__ballot(act) & Q_LEAD);
   STAMP_AT(env, 1);
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
 
   // ---- integrate: drone_swarm_env.py:98-117 (swarm_kernel, DYN_KIN)
   float prev_d = 0.f;
@@ -2460,7 +2471,7 @@ swarm_step16q(const S64Args args) {
   put(act ? 1.f : 0.f);
   wave_sync();
   STAMP_AT(env, 2);
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
 
   // ---- pair + obstacle passes
   uint32_t nk[KS], ok[MSL];
@@ -2475,7 +2486,7 @@ swarm_step16q(const S64Args args) {
   else q16_pair_pass<1, false>(L.soa, d, q, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, esum);
   obstacle_pass_s64<MSL, true>(L.osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
   STAMP_AT(env, 3);
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
 
   // ---- rewards / terminations: drone_swarm_env.py:120-172 (swarm_kernel, DYN_KIN)
   bool pcoll;
@@ -2537,7 +2548,7 @@ swarm_step16q(const S64Args args) {
                                    (do_reset ? SWARM_ENV_RESET : 0u));
   const uint64_t m_term = __ballot(term), m_trunc = __ballot(trunc);
   STAMP_AT(env, 4);
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
 
   // ---- in-kernel auto-reset (wave-uniform): new episode, then its key passes
   uint32_t episode_new = episode0;
@@ -2580,7 +2591,7 @@ swarm_step16q(const S64Args args) {
     dkey = false;  // PASS 0 ranks by s'
   }
   STAMP_AT(env, 5);
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
 
   // ---- exact top-K: quarter q finishes neighbour slot q (q < 3) and obstacle slot q
   const uint32_t nim = ~A->P.nb_keep, oim = ~A->P.ob_keep;
@@ -2651,7 +2662,7 @@ swarm_step16q(const S64Args args) {
     }
   }
   STAMP_AT(env, 6);
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
 
   // ---- state write-back (quarter 0), byte rows from ballots, env scalars (lane 0)
   const bool new_act = do_reset || cont;
@@ -2695,7 +2706,7 @@ swarm_step16q(const S64Args args) {
     if (d == 0) { gs[6 * Q_N + 0] = gx; gs[6 * Q_N + 1] = gy; gs[6 * Q_N + 2] = gz; }
   }
   STAMP_AT(env, 7);
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
 
   // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)], straight from registers
   float* row = A->O.obs + ag * Q_D;
@@ -3068,7 +3079,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   }
   float gx = gx0, gy = gy0, gz = gz0;
   const int n_active = __syncthreads_count(act);
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
 
   // ---- integrate: drone_swarm_env.py:98-117 (swarm_kernel, DYN_KIN)
   float prev_d = 0.f;
@@ -3101,7 +3112,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   }
   h_put(L, w, t, px, py, pz, act ? 1.f : 0.f);
   const bool fast = __syncthreads_and(act) != 0;  // also the barrier after the puts
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
 
   // ---- formation + minimum pass (every pair once), obstacle pass
   double fsum = 0.0;
@@ -3117,7 +3128,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   fsum += (double)L.x.p1.sum[0][i];
   fsum += (double)L.x.p1.sum[1][i];
   smin = fminf(smin, fminf(L.x.p1.mn[0][i], L.x.p1.mn[1][i]));
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
 
   // ---- rewards / terminations: drone_swarm_env.py:120-172 (swarm_kernel, DYN_KIN)
   bool pcoll = smin <= A->P.thr_pair * FAST_LO;
@@ -3148,7 +3159,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   __syncthreads();
   const uint32_t votes = L.red[0] | L.red[1] | L.red[2] | L.red[3];
   const bool any_c = (votes & 1u) != 0, any_cand = (votes & 2u) != 0;
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
   if (n_active == 0) {
     term_all = true;
   } else {
@@ -3209,7 +3220,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     bool c2 = false;
     obstacle_pass_s64<MSL, false>(L.osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
   }
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
   uint32_t nk[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
@@ -3224,7 +3235,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
 #pragma unroll
     for (int s = 0; s < KS; ++s) nk[s] = h_decode(nk[s], w, t, A->P.nb_keep);
   }
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
 
   // ---- exact top-K of the emitted observation (keys rank by s', drone indices)
   float wd[KS], od[MSL];
@@ -3240,7 +3251,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
       if (slow_ob) exact_select<MSL, true>(L.obst, M, -1, H_MS, max_first(od, H_MS), px, py, pz, od, oj);
     }
   }
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
 
   // ---- state write-back
   const bool new_act = do_reset || cont;
@@ -3265,7 +3276,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     gs[3 * H_N + 3 * i] = vx; gs[3 * H_N + 3 * i + 1] = vy; gs[3 * H_N + 3 * i + 2] = vz;
     if (i == 0) { gs[6 * H_N] = gx; gs[6 * H_N + 1] = gy; gs[6 * H_N + 2] = gz; }
   }
-  A = s64_args();
+  SWARM_LAT_REFETCH(A);
 
   // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)], straight from registers
   float* row = A->O.obs + ag * (9 + 4 * H_K + 4 * H_MS);
