@@ -2369,10 +2369,10 @@ __device__ __forceinline__ void q16_pair_pass(const float* __restrict__ soa, int
 #else
 #define Q16_FLAG(f) ((void)0)
 #endif
-// The latency-bound specialisations (step16q, step256: one or four waves per SIMD) read the
-// kernarg segment through one pointer, so the compiler batches the parameter loads at the top
-// instead of a dependent scalar round trip at each phase (step64's per-phase re-fetch keeps the
-// persistent loop's SGPRs free; SWARM_LAT_REFETCH=1 restores it here, diagnostics only).
+// step16q (one wave per SIMD, latency-bound) reads the kernarg segment through one pointer, so
+// the compiler batches the parameter loads at the top instead of a dependent scalar round trip at
+// each phase: 6.85 -> 6.80 us (step256 measured 46.8 -> 47.5-48.2 us that way and keeps step64's
+// per-phase re-fetch; SWARM_LAT_REFETCH_ON=1 restores it here, diagnostics only).
 #ifndef SWARM_LAT_REFETCH_ON
 #define SWARM_LAT_REFETCH_ON 0
 #endif
@@ -3079,7 +3079,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   }
   float gx = gx0, gy = gy0, gz = gz0;
   const int n_active = __syncthreads_count(act);
-  SWARM_LAT_REFETCH(A);
+  A = s64_args();
 
   // ---- integrate: drone_swarm_env.py:98-117 (swarm_kernel, DYN_KIN)
   float prev_d = 0.f;
@@ -3112,7 +3112,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   }
   h_put(L, w, t, px, py, pz, act ? 1.f : 0.f);
   const bool fast = __syncthreads_and(act) != 0;  // also the barrier after the puts
-  SWARM_LAT_REFETCH(A);
+  A = s64_args();
 
   // ---- formation + minimum pass (every pair once), obstacle pass
   double fsum = 0.0;
@@ -3128,7 +3128,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   fsum += (double)L.x.p1.sum[0][i];
   fsum += (double)L.x.p1.sum[1][i];
   smin = fminf(smin, fminf(L.x.p1.mn[0][i], L.x.p1.mn[1][i]));
-  SWARM_LAT_REFETCH(A);
+  A = s64_args();
 
   // ---- rewards / terminations: drone_swarm_env.py:120-172 (swarm_kernel, DYN_KIN)
   bool pcoll = smin <= A->P.thr_pair * FAST_LO;
@@ -3159,7 +3159,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   __syncthreads();
   const uint32_t votes = L.red[0] | L.red[1] | L.red[2] | L.red[3];
   const bool any_c = (votes & 1u) != 0, any_cand = (votes & 2u) != 0;
-  SWARM_LAT_REFETCH(A);
+  A = s64_args();
   if (n_active == 0) {
     term_all = true;
   } else {
@@ -3220,7 +3220,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     bool c2 = false;
     obstacle_pass_s64<MSL, false>(L.osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
   }
-  SWARM_LAT_REFETCH(A);
+  A = s64_args();
   uint32_t nk[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
@@ -3235,7 +3235,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
 #pragma unroll
     for (int s = 0; s < KS; ++s) nk[s] = h_decode(nk[s], w, t, A->P.nb_keep);
   }
-  SWARM_LAT_REFETCH(A);
+  A = s64_args();
 
   // ---- exact top-K of the emitted observation (keys rank by s', drone indices)
   float wd[KS], od[MSL];
@@ -3251,7 +3251,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
       if (slow_ob) exact_select<MSL, true>(L.obst, M, -1, H_MS, max_first(od, H_MS), px, py, pz, od, oj);
     }
   }
-  SWARM_LAT_REFETCH(A);
+  A = s64_args();
 
   // ---- state write-back
   const bool new_act = do_reset || cont;
@@ -3276,7 +3276,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     gs[3 * H_N + 3 * i] = vx; gs[3 * H_N + 3 * i + 1] = vy; gs[3 * H_N + 3 * i + 2] = vz;
     if (i == 0) { gs[6 * H_N] = gx; gs[6 * H_N + 1] = gy; gs[6 * H_N + 2] = gz; }
   }
-  SWARM_LAT_REFETCH(A);
+  A = s64_args();
 
   // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)], straight from registers
   float* row = A->O.obs + ag * (9 + 4 * H_K + 4 * H_MS);
