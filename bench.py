@@ -104,6 +104,14 @@ def parse(argv=None):
     ap.add_argument("--graph", choices=("split", "fused"), default="split",
                     help="env groups in the timed hipGraph: one graph per group stream, or one graph "
                          "holding every group's chain (fork/join captured)")
+    ap.add_argument("--rehearse", type=int, default=3,
+                    help="untimed runs of the whole K-step region (each between device syncs) after the "
+                         "device warm-up, so the timed region follows what it would follow in a loop "
+                         "of such regions, not a 200 ms burst (tools/r03be_cmd.sh: the first region after "
+                         "the burst ran 28.5-29.9 us per step, repeats 26.0-28.0)")
+    ap.add_argument("--region-reps", type=int, default=1,
+                    help="diagnostic: time the K-step region this many times back to back; the line "
+                         "reports the first, `ms_per_step_reps` lists all")
     ap.add_argument("--spin-sync", action="store_true",
                     help="diagnostic: poll the closing event before the closing synchronize")
     ap.add_argument("--graph-short", action="store_true",
@@ -362,9 +370,16 @@ def main(argv=None):
         if args.split_reset:
             split_reset(g)
 
+    # plain env steps with groups: one native call launches every group on its stream
+    # (swarm_step_groups), instead of a Python stream context + launch per group
+    native_groups = G > 1 and pol is None and tracker is None and not args.split_reset
+
     def env_step(k):  # whole batch: group g on group stream g (not joined: groups overlap)
         if G == 1:
             env_step_group(0, k)
+            return
+        if native_groups:
+            vec.step_groups(ring[k % args.ring])
             return
         for g, st in enumerate(vec.group_streams):
             with torch.cuda.stream(st):
@@ -500,17 +515,40 @@ def main(argv=None):
             f" (policy {args.policy} + env step per step)" if pol is not None else "") + (
             " + eval metrics update per group" if tracker is not None else "")
     else:
+        # The device synchronise before t0 already orders the region after every earlier launch,
+        # and the closing one waits for every stream: the group streams need no fork from / join
+        # to a bracket stream (each costs the command processor a barrier packet per stream,
+        # ~15 us per region, tools/k20_intercept.py).  Events on every group stream give the
+        # device time.  A CTDE gather keeps the bracket stream (its side stream joins into it).
+        free = gatherer is None and G > 1
+        ev_free = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(G)] if free else []
+
         def body():
-            t_ev[0].record(stream)
-            fork(t_ev[0])
+            if free:
+                for (e0, _), st in zip(ev_free, vec.group_streams):
+                    e0.record(st)
+            else:
+                t_ev[0].record(stream)
+                fork(t_ev[0])
             for k in range(args.steps):
                 step(k)
-            join()
-            t_ev[1].record(stream)
+            if free:
+                for (_, e1), st in zip(ev_free, vec.group_streams):
+                    e1.record(st)
+            else:
+                join()
+                t_ev[1].record(stream)
         timing = "eager launches" + (f", {G} env groups on {G} HIP streams" if G > 1 else "") + (
             f", CTDE all-gather every {args.gather_every} steps on a side stream ({args.gs_slots}-slot "
             f"global_state ring{', gloo host-staged' if gatherer is not None and gatherer.staged else ''})"
             if gatherer is not None else "")
+    # every event the region records exists before it: torch creates an event's HIP object at
+    # its first record, which would otherwise land inside the timed region (the first region
+    # after the warm-up measured 31.0 us per step against 26.4-28.1 for repeats, --region-reps)
+    for e_ in list(t_ev) + ([e for pair in ev_free for e in pair] if not use_graph else []):
+        e_.record(stream)
+    sync()
     # device warm-up: untimed ring segments until the clocks have ramped (not part of W or K)
     warm_ms, warm_steps = 0.0, 0
     if args.device_warmup_ms > 0:
@@ -535,9 +573,20 @@ def main(argv=None):
                 sync()
         sync()
         warm_ms = (time.perf_counter() - t0) * 1e3
+    if gatherer is None:
+        for _ in range(max(0, args.rehearse)):
+            timed_region(body, world, sync)
     gather_t0 = gatherer.k if gatherer is not None else 0
     wall = timed_region(body, world, sync, spin=t_ev[1] if args.spin_sync else None)
-    kern_ms = t_ev[0].elapsed_time(t_ev[1]) / args.steps
+    walls_rep = [wall]
+    for _ in range(args.region_reps - 1):  # diagnostic repeats (not reported as the value)
+        walls_rep.append(timed_region(body, world, sync))
+    if not use_graph and free:  # first start to last end over the group streams
+        f0 = ev_free[0][0]
+        kern_ms = (max(f0.elapsed_time(e1) for _, e1 in ev_free) -
+                   min(f0.elapsed_time(e0) for e0, _ in ev_free)) / args.steps
+    else:
+        kern_ms = t_ev[0].elapsed_time(t_ev[1]) / args.steps
 
     # ---- diagnostic pass: eager launches, one event pair around every launch on its stream
     # (with env groups the launches of a step overlap: the per-launch mean is what rocprofv3
@@ -623,9 +672,13 @@ def main(argv=None):
         rec = {
             "metric": metric, "value": value, "unit": "agent-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall_max / args.steps * 1e3,
+            **({"ms_per_step_reps": [round(w / args.steps * 1e3, 6) for w in walls_rep]}
+               if args.region_reps > 1 else {}),
             "ms_per_step_eager": eager_max / args.steps * 1e3, "step_timing": timing,
             "device_warmup": {"ms": round(warm_ms, 1), "steps": warm_steps,
-                              "note": "untimed replays after the W warm-up steps, before the timed region"},
+                              "rehearsals": max(0, args.rehearse) if gatherer is None else 0,
+                              "note": "untimed replays after the W warm-up steps, then untimed runs of the "
+                                      "whole K-step region (rehearsals), before the timed region"},
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (device-RNG episodes, uniform(-1,1) actions)",
             "config": {"workload": f"N={n} drones x E={e} envs per GPU, "

@@ -234,6 +234,21 @@ int swarm_step(const swarm_params_t* p, const swarm_state_t* s, const float* act
                const uint8_t* action_mask, const swarm_out_t* o, void* hip_stream);
 
 /*
+ * swarm_step for a batch split into env groups, one launch per group in one call (the batch's
+ * env groups overlap on their streams: one group's launch burst and tail run beside the others'
+ * steady state).  p / s / o / actions / action_mask describe the whole batch of p->num_envs envs;
+ * group g is rows [lo_g, lo_g + group_envs[g]) (lo_g = the sum of the earlier groups), stepped on
+ * hip_streams[g] exactly as swarm_step would step those rows with env_offset + lo_g — results are
+ * bitwise those of one swarm_step over the batch.  group_envs must sum to p->num_envs.  s->work
+ * (persistent kernel only), if set, holds `groups` x SWARM_WORK_WORDS words, one block per group.
+ * No ordering between the streams is added: the caller makes every stream wait for the inputs.
+ * Replaces the per-group Python launch loop (one ctypes call per step instead of G).
+ */
+int swarm_step_groups(const swarm_params_t* p, const swarm_state_t* s, const float* actions,
+                      const uint8_t* action_mask, const swarm_out_t* o, int groups,
+                      const int32_t* group_envs, void* const* hip_streams);
+
+/*
  * Device reset: draw a new episode (Philox4x32-10 keyed by seed, global env index and
  * episode counter) for the envs with env_mask[e] != 0 (NULL = all) and write their obs,
  * dist_goal, global_state.  Outputs of envs not in the mask are left untouched.

@@ -1348,6 +1348,9 @@ __device__ __forceinline__ void pair_group_s64(s64_lds_cf* __restrict__ s0, uint
   float sq[NB], term[NB];
   bool el[NB];
   uint32_t v[NB];
+  // FAST passes with keys send the own key to the mirror (no eligibility flags, no running
+  // minimum, formation travels by DPP): the mirror needs only the key
+  constexpr bool XKEY = FAST && KS > 0;
 #pragma unroll
   for (int i = 0; i + 1 < NB; i += 2) {
     const s64_f2 X = {s0[RT - i], s0[RT - i - 1]};
@@ -1383,9 +1386,20 @@ __device__ __forceinline__ void pair_group_s64(s64_lds_cf* __restrict__ s0, uint
     if constexpr (NB % 2) term[NB - 1] = fabsf(dv[NB - 1] - ds);
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      if constexpr (KS > 0) kins<KS>(nk, (__float_as_uint(dv[i]) & keep) | (uint32_t)(RT - i));
+      if constexpr (KS > 0) {
+        v[i] = (__float_as_uint(dv[i]) & keep) | (uint32_t)(RT - i);
+        kins<KS>(nk, v[i]);
+      } else {
+        v[i] = __float_as_uint(dv[i]);
+      }
       esum += term[i];
-      v[i] = __float_as_uint(dv[i]);
+    }
+  } else if constexpr (XKEY) {
+    // FAST keys-only passes (PASS 0 / 2): the own key, sent as is to the mirror (below)
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      v[i] = (__float_as_uint(pair_value<PASS>(sq[i])) & keep) | (uint32_t)(RT - i);
+      kins<KS>(nk, v[i]);
     }
   } else {
 #pragma unroll
@@ -1398,8 +1412,16 @@ __device__ __forceinline__ void pair_group_s64(s64_lds_cf* __restrict__ s0, uint
     for (int i = 0; i < NB; ++i)
       rc[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t4 + (uint32_t)(256 - 4 * (RT - i))), (int)(v[i] | sflag));
 #pragma unroll
-    for (int i = 0; i < NB; ++i)
-      mirror_pair<KS, PASS, FAST, false>(nk, rc[i], (uint32_t)(64 - RT + i), self, keep_m, ds, smin, esum);
+    for (int i = 0; i < NB; ++i) {
+      if constexpr (XKEY) {
+        // the sender's key with its offset code RT - i swapped for the mirror's 64 - RT + i: one
+        // v_xor_b32 (full rate) instead of v_and_or_b32 on the raw value (same key: the value
+        // is >= 0, so keep and keep_m agree on it)
+        kins<KS>(nk, rc[i] ^ ((uint32_t)(RT - i) ^ (uint32_t)(64 - RT + i)));
+      } else {
+        mirror_pair<KS, PASS, FAST, false>(nk, rc[i], (uint32_t)(64 - RT + i), self, keep_m, ds, smin, esum);
+      }
+    }
     if constexpr (PASS == 1) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) macc = wave_ror1(macc) + term[i];
@@ -3822,6 +3844,60 @@ int swarm_query_launch(const swarm_params_t* p, swarm_launch_info_t* info) {
 int swarm_step(const swarm_params_t* p, const swarm_state_t* s, const float* actions, const uint8_t* action_mask,
                const swarm_out_t* o, void* hip_stream) {
   return launch(MODE_STEP, p, s, actions, action_mask, nullptr, o, hip_stream);
+}
+
+// Env groups in one call: group g = rows [lo_g, lo_g + group_envs[g]) of every [E, ...] buffer,
+// stepped by its own launch on hip_streams[g] with env_offset + lo_g (so its device-RNG draws are
+// those of the whole-batch launch).  The params are validated once, before any group launches.
+int swarm_step_groups(const swarm_params_t* p, const swarm_state_t* s, const float* actions,
+                      const uint8_t* action_mask, const swarm_out_t* o, int groups, const int32_t* group_envs,
+                      void* const* hip_streams) {
+  KParams kp;
+  const int rc0 = build_kparams(p, &kp, nullptr);
+  if (rc0) return rc0;
+  if (!s || !o) return fail(SWARM_ENULL, "state/out is NULL");
+  if (groups < 1) return fail(SWARM_EINVAL, "groups must be >= 1 (got %d)", groups);
+  if (!group_envs || !hip_streams) return fail(SWARM_ENULL, "group_envs/hip_streams is NULL");
+  long long total = 0;
+  for (int g = 0; g < groups; ++g) {
+    if (group_envs[g] < 0) return fail(SWARM_EINVAL, "group_envs[%d] = %d < 0", g, group_envs[g]);
+    total += group_envs[g];
+  }
+  if (total != p->num_envs) return fail(SWARM_EINVAL, "group_envs sum to %lld, num_envs is %d", total, p->num_envs);
+  const size_t N = (size_t)kp.N, M = (size_t)kp.M, D = (size_t)kp.D;
+  size_t lo = 0;
+  for (int g = 0; g < groups; ++g) {
+    auto row = [lo](auto* ptr, size_t per_env) { return ptr ? ptr + lo * per_env : ptr; };
+    swarm_params_t pg = *p;
+    pg.num_envs = group_envs[g];
+    pg.env_offset = p->env_offset + (int64_t)lo;
+    swarm_state_t sg = *s;
+    sg.pos = row(s->pos, 3 * N);
+    sg.vel = row(s->vel, 3 * N);
+    sg.goal = row(s->goal, 3);
+    sg.obstacles = row(s->obstacles, 3 * M);
+    sg.active = row(s->active, N);
+    sg.step_count = row(s->step_count, 1);
+    sg.episode = row(s->episode, 1);
+    sg.damping = row(s->damping, N);
+    sg.work = s->work ? s->work + (size_t)g * SWARM_WORK_WORDS : nullptr;
+    sg.env_cfg = row(s->env_cfg, 1);
+    sg.env_cfg_next = row(s->env_cfg_next, 1);
+    swarm_out_t og = *o;
+    og.obs = row(o->obs, N * D);
+    og.reward = row(o->reward, N);
+    og.terminated = row(o->terminated, N);
+    og.truncated = row(o->truncated, N);
+    og.env_done = row(o->env_done, 1);
+    og.dist_goal = row(o->dist_goal, N);
+    og.info_flags = row(o->info_flags, N);
+    og.global_state = row(o->global_state, 6 * N + 3);
+    const int rc = launch(MODE_STEP, &pg, &sg, row(actions, 3 * N), row(action_mask, N), nullptr, &og,
+                          hip_streams[g]);
+    if (rc) return rc;
+    lo += (size_t)group_envs[g];
+  }
+  return SWARM_OK;
 }
 
 int swarm_reset(const swarm_params_t* p, const swarm_state_t* s, const uint8_t* env_mask, const swarm_out_t* o,

@@ -60,7 +60,7 @@ EVAL_SEGMENTS = 64
 # every symbol include/swarm_mi355x.h declares
 EXPORTED_SYMBOLS = (
     "swarm_abi_version", "swarm_last_error", "swarm_params_default", "swarm_obs_dim",
-    "swarm_query_launch", "swarm_step", "swarm_reset", "swarm_observe",
+    "swarm_query_launch", "swarm_step", "swarm_step_groups", "swarm_reset", "swarm_observe",
     "swarm_policy_packed_bytes", "swarm_policy_pack", "swarm_policy_forward", "swarm_policy_last_error",
     "swarm_eval_begin", "swarm_eval_update", "swarm_eval_single_update", "swarm_eval_last_error",
     "swarm_env_cfg_set",
@@ -187,6 +187,9 @@ def load_library(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.swarm_query_launch.argtypes = [P, ctypes.POINTER(SwarmLaunchInfo)]
     lib.swarm_step.restype = ctypes.c_int
     lib.swarm_step.argtypes = [P, S, vp, vp, O, vp]
+    lib.swarm_step_groups.restype = ctypes.c_int
+    lib.swarm_step_groups.argtypes = [P, S, vp, vp, O, ctypes.c_int, ctypes.POINTER(ctypes.c_int32),
+                                      ctypes.POINTER(ctypes.c_void_p)]
     lib.swarm_reset.restype = ctypes.c_int
     lib.swarm_reset.argtypes = [P, S, vp, O, vp]
     lib.swarm_observe.restype = ctypes.c_int

@@ -157,7 +157,11 @@ class VecSwarm:
                               if g_n > 1 else None)
         self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self._swarm_step = self.lib.swarm_step
+        self._swarm_step_groups = self.lib.swarm_step_groups
         self._gstream_h = [st.cuda_stream for st in self.group_streams] if self.group_streams else []
+        # swarm_step_groups arguments: every group's env count and stream handle
+        self._group_envs_c = (ctypes.c_int32 * g_n)(*[hi - lo for lo, hi in self.group_slices])
+        self._gstreams_c = (ctypes.c_void_p * g_n)(*self._gstream_h) if g_n > 1 else None
         # fork / join events of the group launches, reused by every step (record overwrites)
         self._fork_ev = torch.cuda.Event() if g_n > 1 else None
         self._join_evs = [torch.cuda.Event() for _ in range(g_n)] if g_n > 1 else []
@@ -395,16 +399,45 @@ class VecSwarm:
         cur = torch.cuda.current_stream(self.device)
         fork = self._fork_ev
         fork.record(cur)
-        for g, st in enumerate(self.group_streams):
+        for st in self.group_streams:
             st.wait_event(fork)
-            self._launch_step(g, actions, action_mask, self._gstream_h[g])
             if not join:  # the caller's tensors are in use on the group stream
                 actions.record_stream(st)
                 if action_mask is not None:
                     action_mask.record_stream(st)
+        self._launch_groups(actions, action_mask)
         if join:
             self.join()
         return self.obs, self.reward, self.terminated, self.truncated, self.env_done
+
+    def _launch_groups(self, actions, action_mask) -> None:
+        pr, sr, orf = self._grefs[0]  # group 0's structs hold the batch's row-0 pointers
+        rc = self._swarm_step_groups(ctypes.byref(self.params), sr, actions.data_ptr(),
+                                     None if action_mask is None else action_mask.data_ptr(), orf,
+                                     self.groups, self._group_envs_c, self._gstreams_c)
+        if rc:
+            nat.check(rc, self.lib)
+
+    def step_groups(self, actions: torch.Tensor, action_mask: torch.Tensor | None = None):
+        """One step of all envs, group g launched on group stream g by one native call
+        (swarm_step_groups), with no fork from or join to the current stream: the caller orders
+        the group streams after the inputs (e.g. once per rollout, `fork_groups()`) and before
+        reading the outputs (`join()`).  Group g's steps follow each other on its stream, and
+        groups share no rows, so consecutive steps need no ordering between the streams."""
+        actions, action_mask = self._actions(actions, action_mask)
+        if self.groups == 1:
+            self._launch_step(0, actions, action_mask, self._stream())
+        else:
+            self._launch_groups(actions, action_mask)
+        return self.obs, self.reward, self.terminated, self.truncated, self.env_done
+
+    def fork_groups(self) -> None:
+        """Make every group stream wait for the work issued so far on the current stream."""
+        if self.group_streams is None:
+            return
+        self._fork_ev.record(torch.cuda.current_stream(self.device))
+        for st in self.group_streams:
+            st.wait_event(self._fork_ev)
 
     def step_group(self, g: int, actions: torch.Tensor, action_mask: torch.Tensor | None = None):
         """Step env group `g` only (rows group_slices[g] of the full-batch tensors) on the

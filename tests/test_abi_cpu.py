@@ -202,3 +202,29 @@ def test_env_cfg_set_validation(nat, lib):
     s.env_cfg_next = 64
     assert lib.swarm_step(ctypes.byref(p), ctypes.byref(s), 16, None, ctypes.byref(o), None) == nat.SWARM_ENULL
     assert b"env_cfg" in lib.swarm_last_error()
+
+
+def test_step_groups_validation(nat, lib):
+    """swarm_step_groups checks the params, the group split and its arrays before any launch."""
+    s, o = nat.SwarmState(), nat.SwarmOut()
+    envs = (ctypes.c_int32 * 3)(2, 1, 1)
+    streams = (ctypes.c_void_p * 3)()
+    p = _params(nat, lib, num_envs=4)
+    args = (ctypes.byref(s), None, None, ctypes.byref(o))
+    assert lib.swarm_step_groups(None, *args, 3, envs, streams) == nat.SWARM_ENULL
+    assert lib.swarm_step_groups(ctypes.byref(p), None, None, None, ctypes.byref(o), 3, envs, streams) == nat.SWARM_ENULL
+    assert lib.swarm_step_groups(ctypes.byref(p), *args, 0, envs, streams) == nat.SWARM_EINVAL
+    assert lib.swarm_step_groups(ctypes.byref(p), *args, 3, None, streams) == nat.SWARM_ENULL
+    assert lib.swarm_step_groups(ctypes.byref(p), *args, 3, envs, None) == nat.SWARM_ENULL
+    assert lib.swarm_step_groups(ctypes.byref(p), *args, 2, envs, streams) == nat.SWARM_EINVAL  # 3 != 4 envs
+    assert b"sum" in lib.swarm_last_error()
+    neg = (ctypes.c_int32 * 3)(5, -1, 0)
+    assert lib.swarm_step_groups(ctypes.byref(p), *args, 3, neg, streams) == nat.SWARM_EINVAL
+    bad = _params(nat, lib, num_envs=4, num_drones=0)
+    assert lib.swarm_step_groups(ctypes.byref(bad), *args, 3, envs, streams) == nat.SWARM_ELIMIT
+    # the split is valid, the buffers are not: the first group's launch rejects them
+    assert lib.swarm_step_groups(ctypes.byref(p), *args, 3, envs, streams) == nat.SWARM_ENULL
+    # zero envs in every group: a valid no-op
+    p0 = _params(nat, lib, num_envs=0)
+    zero = (ctypes.c_int32 * 2)(0, 0)
+    assert lib.swarm_step_groups(ctypes.byref(p0), *args, 2, zero, streams) == 0

@@ -97,3 +97,23 @@ def test_groups_validation(dev):
     v = VecSwarm(4, {"num_drones": 8}, device=dev, groups=2)
     with pytest.raises(ValueError):
         v.step_group(2, torch.zeros((4, 8, 3), device=dev))
+
+
+@pytest.mark.parametrize("e,n,g,kw", [(8192, 64, 4, {}), (1000, 16, 3, {}), (96, 256, 2, {}),
+                                      (300, 64, 3, {"dynamics": "physics"}), (77, 5, 4, {})])
+def test_step_groups_native_launch(dev, e, n, g, kw):
+    """VecSwarm.step_groups (swarm_step_groups: one native call, group g on stream g, no fork or
+    join per step) equals single launches bitwise, with and without an action mask."""
+    a, b = _pair(dev, e, n, g, **kw)
+    acts = [_acts(dev, e, n, k) for k in range(6)]
+    gm = torch.Generator(device=dev).manual_seed(77)
+    masks = [None if k % 2 == 0 else (torch.rand((e, n), device=dev, generator=gm) < 0.8).to(torch.uint8)
+             for k in range(6)]
+    torch.cuda.synchronize()
+    b.fork_groups()
+    for k in range(6):
+        a.step(acts[k], masks[k])
+        b.step_groups(acts[k], masks[k])
+    b.join()
+    torch.cuda.synchronize()
+    _same(a, b, "step_groups")
