@@ -1391,6 +1391,7 @@ __device__ __forceinline__ void pair_group_s64(s64_lds_cf* __restrict__ s0, uint
         kins<KS>(nk, v[i]);
       } else {
         v[i] = __float_as_uint(dv[i]);
+        smin = fminf(smin, dv[i]);  // no keys: the running minimum decides pair collisions
       }
       esum += term[i];
     }
@@ -1755,6 +1756,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   float smin = __builtin_inff();
   double fsum = 0.0;
   const bool fast = DYN == DYN_PHYS || __all(act);
+  bool early = false;  // kinematic: the episode ends whatever the pair pass finds (no keys needed)
 #if SWARM_DIAG_EXTRA_VALU
   {  // diagnostic: SWARM_DIAG_EXTRA_VALU dependent-free FAST VALU ops per wave
     float z0 = px, z1 = py, z2 = pz, z3 = px + 1.f;
@@ -1769,18 +1771,30 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     pair_pass_s64<KS, 2, true>(soa, t, px, py, pz, true, A->P.nb_keep, 0.f, nk, smin, fsum);
     obstacle_pass_s64<MSL, true>(osoa, M, px, py, pz, true, A->P.s_phys_obst, A->P.ob_keep, ok, ocoll);
   } else {
-#if SWARM_DIAG_NO_FORMATION
-    if (fast) pair_pass_s64<KS, 0, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
-#else
-    if (fast) pair_pass_s64<KS, 1, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
-#endif
-    else pair_pass_s64<KS, 1, false>(soa, t, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
+    // obstacle pass first: an obstacle collision (or the time limit) ends the episode whatever
+    // the pair pass finds, so such an env — ~half of the resetting ones — runs the pair pass
+    // without neighbour keys (they would rank the positions the reset replaces): formation terms
+    // and the running minimum only, the same sums bit for bit
     if (SWARM_ABLATE & ABL_OBST) {  // diagnostic: obstacle collisions only, no obstacle keys
       uint32_t ok0[1];
       obstacle_pass_s64<0, true>(osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok0, ocoll);
     } else {
       obstacle_pass_s64<MSL, true>(osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
     }
+    A = s64_args();
+    early = fast && A->P.auto_reset && !(SWARM_ABLATE & ABL_RESET) &&
+            (__ballot(act && ocoll) != 0 || stepc + 1 >= A->P.max_steps);
+#if SWARM_DIAG_NO_FORMATION
+    if (fast) pair_pass_s64<KS, 0, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
+#else
+    if (early) {
+      uint32_t nk0[1] = {KEY_EMPTY};
+      pair_pass_s64<0, 1, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk0, smin, fsum);
+    } else if (fast) {
+      pair_pass_s64<KS, 1, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
+    }
+#endif
+    else pair_pass_s64<KS, 1, false>(soa, t, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
   }
   if constexpr (LANDED) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next env's inputs are in
   STAMP_AT(srec, 3);
@@ -1852,7 +1866,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     trunc = trunc_all;
     cont = true;
   } else {
-    if (fast) {
+    if (fast && !early) {
       const uint32_t keep = A->P.nb_keep;
       pcoll = __uint_as_float(nk[0] | ~keep) * FAST_HI <= A->P.thr_pair;
       if (!pcoll && __uint_as_float(nk[0] & keep) * FAST_LO <= A->P.thr_pair)
