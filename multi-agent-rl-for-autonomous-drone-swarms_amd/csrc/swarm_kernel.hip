@@ -2939,21 +2939,22 @@ __device__ __forceinline__ void h_seg0(s64_lds_cf* __restrict__ P0, s64_lds_cf* 
       s[0] = sqsum_rank(X[r] - px, Y[r] - py, Z[r] - pz);
       s[1] = 0.f;
     }
-    uint32_t rc[2] = {0u, 0u};
-    if constexpr (MIRROR) {
+    // the own key goes to the mirror as is; the mirror swaps its code CO + r for CM + (64 - r) % 64
+    // with one full-rate v_xor_b32 (s' >= 0: the sign bit is clear on both sides)
+    uint32_t key[2] = {0u, 0u}, rc[2] = {0u, 0u};
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h == 1 && !two) break;
-        rc[h] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t4 + (uint32_t)(256 - 4 * (r - h))),
-                                                       (int)__float_as_uint(s[h]));
-      }
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !two) break;
+      key[h] = (__float_as_uint(s[h]) & keepv) | (uint32_t)(CO + r - h);
+      if constexpr (MIRROR)
+        rc[h] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(t4 + (uint32_t)(256 - 4 * (r - h))), (int)key[h]);
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if (h == 1 && !two) break;
       const int rr = r - h;
-      kins<4>(nk, (__float_as_uint(s[h]) & keepv) | (uint32_t)(CO + rr));
-      if constexpr (MIRROR) kins<4>(mk, (rc[h] & keepv) | (uint32_t)(CM + ((64 - rr) & 63)));
+      kins<4>(nk, key[h]);
+      if constexpr (MIRROR) kins<4>(mk, rc[h] ^ ((uint32_t)(CO + rr) ^ (uint32_t)(CM + ((64 - rr) & 63))));
     }
     if (((RHI - r) % H_BATCH) == H_BATCH - 2) __builtin_amdgcn_sched_barrier(0);
   }
