@@ -65,6 +65,8 @@
 #define ABL_RESET_WORK 1024 // step64: a resetting env draws its new state but skips its key passes,
                             // finish and obs (wrong obs; the dynamics are unchanged)
 #define ABL_EXACT 2048      // sqrt_rn = v_sqrt_f32 and the sdot norm in f32 (inexact; timing only)
+#define ABL_GENERAL 4096    // step64: never run the general finish (near-tie waves keep the fast answer)
+#define ABL_PHILOX 8192     // step64: reset draws from one multiply-xor per word instead of Philox
 
 // Diagnostic phase timestamps (tools/stamps.py; never set in the product build)
 #ifdef SWARM_STAMPS
@@ -583,26 +585,42 @@ __device__ __forceinline__ float max_first(const float (&arr)[S], int K) {
 // K-th of the re-ranked survivors), so only points whose f32 squared sum lies within dmax^2 (plus
 // the f32 error band) can belong to the answer: a cheap scan filters, and the exact distance is
 // evaluated only for those few.
+#ifndef SWARM_FB_BATCH
+#define SWARM_FB_BATCH 8
+#endif
 template <int S, bool AXIS>
 __device__ __forceinline__ void exact_select(const float4* __restrict__ pts, int count, int self, int K, float dmax,
                                              float px, float py, float pz, float (&wd)[S], int (&wj)[S]) {
 #pragma unroll
   for (int u = 0; u < S; ++u) { wd[u] = __builtin_inff(); wj[u] = 0x7fffffff; }
   const float s_cut = (dmax * dmax) * FAST_HI;
-  for (int j = 0; j < count; ++j) {
-    const float4 q = pts[j];
-    const float sq = sqsum_f(q.x - px, q.y - py, q.z - pz);
-    if (j != self && sq <= s_cut) {
-      float cd = AXIS ? sqrt_rn(sq) : sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
-      int cj = j;
+  // batches of 8 points: the batch's LDS reads are issued together and its filter sums computed
+  // before the first (divergent) exact evaluation, instead of one exposed LDS round trip per
+  // point — a wave in this fallback is the last of its launch more often than not
+  constexpr int B = SWARM_FB_BATCH;
+#pragma unroll 1
+  for (int j0 = 0; j0 < count; j0 += B) {
+    float4 q[B];
+    float sq[B];
 #pragma unroll
-      for (int u = 0; u < S; ++u) {  // insertion by exchange: the largest falls off slot K-1
-        if (u < K) {
-          const bool lt = (cd < wd[u]) || (cd == wd[u] && cj < wj[u]);
-          const float td = wd[u];
-          const int tj = wj[u];
-          wd[u] = lt ? cd : td; wj[u] = lt ? cj : tj;
-          cd = lt ? td : cd; cj = lt ? tj : cj;
+    for (int u = 0; u < B; ++u) q[u] = pts[j0 + u < count ? j0 + u : j0];
+#pragma unroll
+    for (int u = 0; u < B; ++u) sq[u] = sqsum_f(q[u].x - px, q[u].y - py, q[u].z - pz);
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int j = j0 + u;
+      if (j < count && j != self && sq[u] <= s_cut) {
+        float cd = AXIS ? sqrt_rn(sq[u]) : sqrt_rn(sqsum_1d(q[u].x - px, q[u].y - py, q[u].z - pz));
+        int cj = j;
+#pragma unroll
+        for (int v = 0; v < S; ++v) {  // insertion by exchange: the largest falls off slot K-1
+          if (v < K) {
+            const bool lt = (cd < wd[v]) || (cd == wd[v] && cj < wj[v]);
+            const float td = wd[v];
+            const int tj = wj[v];
+            wd[v] = lt ? cd : td; wj[v] = lt ? cj : tj;
+            cd = lt ? td : cd; cj = lt ? tj : cj;
+          }
         }
       }
     }
@@ -625,10 +643,18 @@ __device__ __forceinline__ bool exact_pair_collision(const float4* __restrict__ 
                                                      float px, float py, float pz, float s_thr) {
   bool c = false;
   const float s_cut = s_thr * FAST_HI;
-  for (int j = 0; j < count; ++j) {
-    const float4 q = pts[j];
-    if (j != self && q.w != 0.f && sqsum_f(q.x - px, q.y - py, q.z - pz) <= s_cut)
-      c = c || (sqsum_1d(q.x - px, q.y - py, q.z - pz) <= s_thr);
+  constexpr int B = SWARM_FB_BATCH;  // batched LDS reads, as exact_select
+#pragma unroll 1
+  for (int j0 = 0; j0 < count; j0 += B) {
+    float4 q[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) q[u] = pts[j0 + u < count ? j0 + u : j0];
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int j = j0 + u;
+      if (j < count && j != self && q[u].w != 0.f && sqsum_f(q[u].x - px, q[u].y - py, q[u].z - pz) <= s_cut)
+        c = c || (sqsum_1d(q[u].x - px, q[u].y - py, q[u].z - pz) <= s_thr);
+    }
   }
   return c;
 }
@@ -1523,22 +1549,25 @@ __device__ __forceinline__ void s64_put(float4* __restrict__ ring, float* __rest
 // whenever no two survivors are a near-tie and the survivor bound holds.  Returns false for a
 // lane that needs the general finish (finish_keys + exact_select); the caller runs that for the
 // whole wave when any lane does (its answer for the other lanes is the same).
+// Flags of s64_finish_fast (per lane): a near-tie among the neighbour / obstacle survivors, and
+// the survivor bound failing on either side.
+constexpr uint32_t S64F_NEAR_NB = 1u, S64F_NEAR_OB = 2u, S64F_BOUND_NB = 4u, S64F_BOUND_OB = 8u;
 template <int KS, int MSL>
-__device__ __forceinline__ bool s64_finish_fast(const uint32_t (&nk)[KS], const uint32_t (&ok)[MSL],
-                                                const float4* __restrict__ ring, const float4* __restrict__ obst,
-                                                int t, int M, uint32_t nb_keep, uint32_t ob_keep, bool dkey,
-                                                float px, float py, float pz, float (&wd)[KS], int (&wj)[KS],
-                                                float (&od)[MSL], int (&oj)[MSL]) {
+__device__ __forceinline__ uint32_t s64_finish_fast(const uint32_t (&nk)[KS], const uint32_t (&ok)[MSL],
+                                                    const float4* __restrict__ ring, const float4* __restrict__ obst,
+                                                    int t, int M, uint32_t nb_keep, uint32_t ob_keep, bool dkey,
+                                                    float px, float py, float pz, float (&wd)[KS], int (&wj)[KS],
+                                                    float (&od)[MSL], int (&oj)[MSL]) {
   constexpr int K = KS - 1, MS = MSL - 1;
   const uint32_t nim = ~nb_keep, oim = ~ob_keep;
-  bool near = false;
+  bool near_nb = false, near_ob = false;
 #pragma unroll
   for (int s = 0; s + 1 < KS; ++s)
-    near = near | (__uint_as_float(nk[s + 1] & nb_keep) <= __uint_as_float((nk[s] & nb_keep) | nim) * FAST_HI);
+    near_nb = near_nb | (__uint_as_float(nk[s + 1] & nb_keep) <= __uint_as_float((nk[s] & nb_keep) | nim) * FAST_HI);
 #pragma unroll
   for (int s = 0; s + 1 < MSL; ++s)
-    near = near | ((ok[s + 1] != KEY_EMPTY) &
-                   (__uint_as_float(ok[s + 1] & ob_keep) <= __uint_as_float((ok[s] & ob_keep) | oim) * FAST_HI));
+    near_ob = near_ob | ((ok[s + 1] != KEY_EMPTY) &
+                         (__uint_as_float(ok[s + 1] & ob_keep) <= __uint_as_float((ok[s] & ob_keep) | oim) * FAST_HI));
 #pragma unroll
   for (int s = 0; s < K; ++s) {
     const int j = (t + (int)(nk[s] & nim)) & (S64_N - 1);
@@ -1565,7 +1594,72 @@ __device__ __forceinline__ bool s64_finish_fast(const uint32_t (&nk)[KS], const 
   const float wo = od[MS - 1];
   const bool ok_ob = last == KEY_EMPTY || (int)(last & oim) >= M ||
                      __uint_as_float(last & ob_keep) > (wo * wo) * FAST_HI;
-  return !near && ok_nb && ok_ob;
+  return (near_nb ? S64F_NEAR_NB : 0u) | (near_ob ? S64F_NEAR_OB : 0u) | (ok_nb ? 0u : S64F_BOUND_NB) |
+         (ok_ob ? 0u : S64F_BOUND_OB);
+}
+
+// The rest of finish_keys for the lanes s64_finish_fast flagged, straight-line (finish_keys'
+// per-slot validity branches serialise its exact-distance chains, and a wave in this path tends
+// to be its launch's last): the exact distances of slots 0 .. K-1 / 0 .. MS-1 are s64_finish_fast's
+// (the same formulas); a near-tie adds the last slot's and re-sorts all slots by (distance,
+// index); then finish_keys' survivor bound on the sorted list.  Returns the lanes' (slow_nb,
+// slow_ob): their answer needs exact_select.  Same results as finish_keys, slot for slot.
+template <int KS, int MSL>
+__device__ __forceinline__ void s64_finish_general(uint32_t flags, const uint32_t (&nk)[KS], const uint32_t (&ok)[MSL],
+                                                   const float4* __restrict__ ring, const float4* __restrict__ obst,
+                                                   int t, int M, uint32_t nb_keep, uint32_t ob_keep, bool dkey,
+                                                   float px, float py, float pz, float (&wd)[KS], int (&wj)[KS],
+                                                   float (&od)[MSL], int (&oj)[MSL], bool& slow_nb, bool& slow_ob) {
+  constexpr int K = KS - 1, MS = MSL - 1;
+  const uint32_t nim = ~nb_keep, oim = ~ob_keep;
+  const bool near_nb = (flags & S64F_NEAR_NB) != 0, near_ob = (flags & S64F_NEAR_OB) != 0;
+  if (__ballot(near_nb) != 0) {
+    const int j = (t + (int)(nk[K] & nim)) & (S64_N - 1);  // N = 64 > K: slot K is always a drone
+    const float4 q = ring[j];
+    const float d = sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
+    if (near_nb) {
+      wd[K] = d;
+      wj[K] = j;
+#pragma unroll
+      for (int a = 1; a < KS; ++a)
+#pragma unroll
+        for (int r = a; r > 0; --r) {
+          const float x = wd[r - 1], y = wd[r];
+          const int jx = wj[r - 1], jy = wj[r];
+          const bool sw = (y < x) || (y == x && jy < jx);
+          wd[r - 1] = sw ? y : x; wd[r] = sw ? x : y;
+          wj[r - 1] = sw ? jy : jx; wj[r] = sw ? jx : jy;
+        }
+    }
+  }
+  if (__ballot(near_ob) != 0) {
+    const uint32_t key = ok[MS];
+    const int j = (int)(key & oim);
+    const bool valid = key != KEY_EMPTY && j < M;
+    const float4 q = obst[j & (S64_MMAX - 1)];
+    const float d = sqrt_rn(sqsum_f(q.x - px, q.y - py, q.z - pz));
+    if (near_ob) {
+      od[MS] = valid ? d : __builtin_inff();
+      oj[MS] = valid ? j : 0x7fffffff;
+#pragma unroll
+      for (int a = 1; a < MSL; ++a)
+#pragma unroll
+        for (int r = a; r > 0; --r) {
+          const float x = od[r - 1], y = od[r];
+          const int jx = oj[r - 1], jy = oj[r];
+          const bool sw = (y < x) || (y == x && jy < jx);
+          od[r - 1] = sw ? y : x; od[r] = sw ? x : y;
+          oj[r - 1] = sw ? jy : jx; oj[r] = sw ? jx : jy;
+        }
+    }
+  }
+  // finish_keys' bound: the last key bounds every non-survivor (N = 64 > KS: it is a drone)
+  const float nb_base = __uint_as_float(nk[K] & nb_keep);
+  const float w = wd[K - 1];
+  slow_nb = !(dkey ? nb_base * FAST_LO > w : nb_base * FAST_LO > (w * w) * FAST_HI);
+  const uint32_t last = ok[MS];
+  const float wo = od[MS - 1];
+  slow_ob = !(last == KEY_EMPTY || (int)(last & oim) >= M || __uint_as_float(last & ob_keep) > (wo * wo) * FAST_HI);
 }
 
 // One env's inputs, loaded one env ahead of its compute (software pipeline): raw loaded values
@@ -1811,13 +1905,29 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       for (int s = 0; s < MSL; ++s) { od[s] = __uint_as_float(ok[s] & A->P.ob_keep); oj[s] = (int)(ok[s] & 15u); }
       return;
     }
-    if (__ballot(!s64_finish_fast<KS, MSL>(nk, ok, ring, obst, t, M, A->P.nb_keep, A->P.ob_keep, dkey, px, py, pz, wd,
-                                           wj, od, oj)) == 0)
-      return;
-    const bool slow_nb = !finish_keys<KS, false, true>(nk, ring, S64_N, t, S64_N - 1, S64_K, A->P.nb_keep, dkey, px, py,
-                                                       pz, wd, wj);
-    const bool slow_ob = !finish_keys<MSL, true, false>(ok, obst, M, 0, 0x7fffffff, S64_MS, A->P.ob_keep, false, px, py,
-                                                        pz, od, oj);
+    const uint32_t fflags = s64_finish_fast<KS, MSL>(nk, ok, ring, obst, t, M, A->P.nb_keep, A->P.ob_keep, dkey, px, py,
+                                                     pz, wd, wj, od, oj);
+    const uint64_t fails = __ballot(fflags != 0);
+#ifdef SWARM_DIAG_FINISH  // diagnostic counters (stamps build): waves / lanes through the general finish
+    if (t == 0) {
+      atomicAdd(&g_stamps[(1 << 19) + 0], 1ull);
+      if (fails) { atomicAdd(&g_stamps[(1 << 19) + 1], 1ull); atomicAdd(&g_stamps[(1 << 19) + 2], (unsigned long long)__popcll(fails)); }
+    }
+#endif
+    if (fails == 0 || (SWARM_ABLATE & ABL_GENERAL)) return;
+    bool slow_nb, slow_ob;
+    s64_finish_general<KS, MSL>(fflags, nk, ok, ring, obst, t, M, A->P.nb_keep, A->P.ob_keep, dkey, px, py, pz, wd, wj,
+                                od, oj, slow_nb, slow_ob);
+#ifdef SWARM_DIAG_FINISH
+    {
+      const uint64_t bn = __ballot(slow_nb), bo = __ballot(slow_ob);
+      if (t == 0) {
+        if (bn) { atomicAdd(&g_stamps[(1 << 19) + 3], 1ull); atomicAdd(&g_stamps[(1 << 19) + 4], (unsigned long long)__popcll(bn)); }
+        if (bo) { atomicAdd(&g_stamps[(1 << 19) + 5], 1ull); atomicAdd(&g_stamps[(1 << 19) + 6], (unsigned long long)__popcll(bo)); }
+        if (!dkey) atomicAdd(&g_stamps[(1 << 19) + 7], 1ull);
+      }
+    }
+#endif
     if (slow_nb) exact_select<KS, false>(ring, S64_N, t, S64_K, max_first(wd, S64_K), px, py, pz, wd, wj);
     if (slow_ob) exact_select<MSL, true>(obst, M, -1, S64_MS, max_first(od, S64_MS), px, py, pz, od, oj);
   };
@@ -1927,8 +2037,14 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     // two independent Philox chains per lane: drone t (block t), and obstacle t (block N + t) for
     // lanes t < M / the goal (block N + M) on lane M
     uint32_t w[4], wo[4];
-    draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)t, w);
-    draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)(S64_N + (t < M ? t : M)), wo);
+    if (SWARM_ABLATE & ABL_PHILOX) {  // diagnostic: cheap stand-in draws (wrong values)
+      const uint32_t h0 = ((uint32_t)t + episode_new * 0x9E3779B9u) * 0x85EBCA6Bu ^ (uint32_t)genv;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { w[k] = h0 * (2u * k + 1u); wo[k] = (h0 ^ 0x55u) * (2u * k + 3u); }
+    } else {
+      draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)t, w);
+      draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)(S64_N + (t < M ? t : M)), wo);
+    }
     const float lo_w = A->P.neg_half_w, wd_w = A->P.width_w;
     px = uni(w[0], lo_w, wd_w);
     py = uni(w[1], lo_w, wd_w);
@@ -1960,11 +2076,11 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       double f2 = 0.0;
       pair_pass_s64<KS, 0, true>(soa, t, px, py, pz, true, A->P.nb_keep, 0.f, nk, s2, f2);
       if (!(SWARM_ABLATE & ABL_OBST)) obstacle_pass_s64<MSL, false>(osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
-      select_topk(false);
     }
-  } else {
-    select_topk(DYN == DYN_KIN);  // the kinematic step pass ranks by d~, physics by s'
   }
+  // one call site for both (the new episode's s' keys, the kinematic step pass's d~ keys; physics
+  // ranks by s'): the finish and its general fallback are emitted once, not once per branch
+  if (!(do_reset && (SWARM_ABLATE & ABL_RESET_WORK))) select_topk(DYN == DYN_KIN && !do_reset);
 
   STAMP_AT(srec, 6);
   A = s64_args();
