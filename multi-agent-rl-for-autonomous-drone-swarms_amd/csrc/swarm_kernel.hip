@@ -1604,7 +1604,9 @@ __device__ __forceinline__ uint32_t s64_finish_fast(const uint32_t (&nk)[KS], co
 // (the same formulas); a near-tie adds the last slot's and re-sorts all slots by (distance,
 // index); then finish_keys' survivor bound on the sorted list.  Returns the lanes' (slow_nb,
 // slow_ob): their answer needs exact_select.  Same results as finish_keys, slot for slot.
-template <int KS, int MSL>
+// NR drones in `ring`; ROT: neighbour keys carry an offset from drone t (step64), else the drone
+// index (step256); MMAX obstacle slots in `obst`.
+template <int KS, int MSL, int NR = S64_N, bool ROT = true, int MMAX = S64_MMAX>
 __device__ __forceinline__ void s64_finish_general(uint32_t flags, const uint32_t (&nk)[KS], const uint32_t (&ok)[MSL],
                                                    const float4* __restrict__ ring, const float4* __restrict__ obst,
                                                    int t, int M, uint32_t nb_keep, uint32_t ob_keep, bool dkey,
@@ -1614,7 +1616,8 @@ __device__ __forceinline__ void s64_finish_general(uint32_t flags, const uint32_
   const uint32_t nim = ~nb_keep, oim = ~ob_keep;
   const bool near_nb = (flags & S64F_NEAR_NB) != 0, near_ob = (flags & S64F_NEAR_OB) != 0;
   if (__ballot(near_nb) != 0) {
-    const int j = (t + (int)(nk[K] & nim)) & (S64_N - 1);  // N = 64 > K: slot K is always a drone
+    // N > KS: slot K is always a drone
+    const int j = ((ROT ? t : 0) + (int)(nk[K] & nim)) & (NR - 1);
     const float4 q = ring[j];
     const float d = sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
     if (near_nb) {
@@ -1636,7 +1639,7 @@ __device__ __forceinline__ void s64_finish_general(uint32_t flags, const uint32_
     const uint32_t key = ok[MS];
     const int j = (int)(key & oim);
     const bool valid = key != KEY_EMPTY && j < M;
-    const float4 q = obst[j & (S64_MMAX - 1)];
+    const float4 q = obst[j & (MMAX - 1)];
     const float d = sqrt_rn(sqsum_f(q.x - px, q.y - py, q.z - pz));
     if (near_ob) {
       od[MS] = valid ? d : __builtin_inff();
@@ -3159,20 +3162,21 @@ __device__ __forceinline__ uint32_t h_decode(uint32_t key, int w, int t, uint32_
 }
 
 // step64's straight-line finish (s64_finish_fast) with drone indices in the neighbour keys
-__device__ __forceinline__ bool h_finish_fast(const uint32_t (&nk)[4], const uint32_t (&ok)[5],
-                                              const float4* __restrict__ ring, const float4* __restrict__ obst, int M,
-                                              uint32_t nb_keep, uint32_t ob_keep, float px, float py, float pz,
-                                              float (&wd)[4], int (&wj)[4], float (&od)[5], int (&oj)[5]) {
+__device__ __forceinline__ uint32_t h_finish_fast(const uint32_t (&nk)[4], const uint32_t (&ok)[5],
+                                                  const float4* __restrict__ ring, const float4* __restrict__ obst,
+                                                  int M, uint32_t nb_keep, uint32_t ob_keep, float px, float py,
+                                                  float pz, float (&wd)[4], int (&wj)[4], float (&od)[5],
+                                                  int (&oj)[5]) {
   constexpr int K = 3, MS = 4;
   const uint32_t nim = ~nb_keep, oim = ~ob_keep;
-  bool near = false;
+  bool near_nb = false, near_ob = false;
 #pragma unroll
   for (int s = 0; s + 1 < 4; ++s)
-    near = near | (__uint_as_float(nk[s + 1] & nb_keep) <= __uint_as_float((nk[s] & nb_keep) | nim) * FAST_HI);
+    near_nb = near_nb | (__uint_as_float(nk[s + 1] & nb_keep) <= __uint_as_float((nk[s] & nb_keep) | nim) * FAST_HI);
 #pragma unroll
   for (int s = 0; s + 1 < 5; ++s)
-    near = near | ((ok[s + 1] != KEY_EMPTY) &
-                   (__uint_as_float(ok[s + 1] & ob_keep) <= __uint_as_float((ok[s] & ob_keep) | oim) * FAST_HI));
+    near_ob = near_ob | ((ok[s + 1] != KEY_EMPTY) &
+                         (__uint_as_float(ok[s + 1] & ob_keep) <= __uint_as_float((ok[s] & ob_keep) | oim) * FAST_HI));
 #pragma unroll
   for (int s = 0; s < K; ++s) {
     const int j = (int)(nk[s] & nim) & (H_N - 1);
@@ -3199,7 +3203,8 @@ __device__ __forceinline__ bool h_finish_fast(const uint32_t (&nk)[4], const uin
   const float wo = od[MS - 1];
   const bool ok_ob = last == KEY_EMPTY || (int)(last & oim) >= M ||
                      __uint_as_float(last & ob_keep) > (wo * wo) * FAST_HI;
-  return !near && ok_nb && ok_ob;
+  return (near_nb ? S64F_NEAR_NB : 0u) | (near_ob ? S64F_NEAR_OB : 0u) | (ok_nb ? 0u : S64F_BOUND_NB) |
+         (ok_ob ? 0u : S64F_BOUND_OB);
 }
 
 #if SWARM_HAS_PART(7)  // emitted in its own translation unit only
@@ -3394,12 +3399,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   float wd[KS], od[MSL];
   int wj[KS], oj[MSL];
   {
-    const bool okf = h_finish_fast(nk, ok, L.ring, L.obst, M, A->P.nb_keep, A->P.ob_keep, px, py, pz, wd, wj, od, oj);
-    if (__builtin_expect(!okf, 0)) {
-      const bool slow_nb = !finish_keys<KS, false, true>(nk, L.ring, H_N, 0, H_N - 1, H_K, A->P.nb_keep, false, px, py,
-                                                         pz, wd, wj);
-      const bool slow_ob = !finish_keys<MSL, true, false>(ok, L.obst, M, 0, 0x7fffffff, H_MS, A->P.ob_keep, false, px,
-                                                          py, pz, od, oj);
+    const uint32_t ff = h_finish_fast(nk, ok, L.ring, L.obst, M, A->P.nb_keep, A->P.ob_keep, px, py, pz, wd, wj, od, oj);
+    if (__ballot(ff != 0) != 0) {  // straight-line rest of finish_keys (s64_finish_general), then the scans
+      bool slow_nb, slow_ob;
+      s64_finish_general<KS, MSL, H_N, false, H_MMAX>(ff, nk, ok, L.ring, L.obst, i, M, A->P.nb_keep, A->P.ob_keep,
+                                                      false, px, py, pz, wd, wj, od, oj, slow_nb, slow_ob);
       if (slow_nb) exact_select<KS, false>(L.ring, H_N, i, H_K, max_first(wd, H_K), px, py, pz, wd, wj);
       if (slow_ob) exact_select<MSL, true>(L.obst, M, -1, H_MS, max_first(od, H_MS), px, py, pz, od, oj);
     }
