@@ -67,6 +67,8 @@
 #define ABL_EXACT 2048      // sqrt_rn = v_sqrt_f32 and the sdot norm in f32 (inexact; timing only)
 #define ABL_GENERAL 4096    // step64: never run the general finish (near-tie waves keep the fast answer)
 #define ABL_PHILOX 8192     // step64: reset draws from one multiply-xor per word instead of Philox
+#define ABL_EXSEL 16384     // step64: the general finish without exact_select (its answer kept)
+#define ABL_GENKEEP 32768   // step64: the fast finish's checks and ballot kept, the general finish skipped
 
 // Diagnostic phase timestamps (tools/stamps.py; never set in the product build)
 #ifdef SWARM_STAMPS
@@ -587,6 +589,9 @@ __device__ __forceinline__ float max_first(const float (&arr)[S], int K) {
 // evaluated only for those few.
 #ifndef SWARM_FB_BATCH
 #define SWARM_FB_BATCH 8
+#endif
+#ifndef SWARM_FB_PRIO
+#define SWARM_FB_PRIO 0
 #endif
 template <int S, bool AXIS>
 __device__ __forceinline__ void exact_select(const float4* __restrict__ pts, int count, int self, int K, float dmax,
@@ -1917,7 +1922,12 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       if (fails) { atomicAdd(&g_stamps[(1 << 19) + 1], 1ull); atomicAdd(&g_stamps[(1 << 19) + 2], (unsigned long long)__popcll(fails)); }
     }
 #endif
+    if (SWARM_ABLATE & ABL_GENKEEP) {  // diagnostic: keep the checks alive, never take the general path
+      if (fails == 0x123456789abcdefull) wd[0] = 0.f;
+      return;
+    }
     if (fails == 0 || (SWARM_ABLATE & ABL_GENERAL)) return;
+    if constexpr (SWARM_FB_PRIO > 0) __builtin_amdgcn_s_setprio(SWARM_FB_PRIO);  // a fallback wave is its launch's last
     bool slow_nb, slow_ob;
     s64_finish_general<KS, MSL>(fflags, nk, ok, ring, obst, t, M, A->P.nb_keep, A->P.ob_keep, dkey, px, py, pz, wd, wj,
                                 od, oj, slow_nb, slow_ob);
@@ -1931,6 +1941,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       }
     }
 #endif
+    if (SWARM_ABLATE & ABL_EXSEL) return;
     if (slow_nb) exact_select<KS, false>(ring, S64_N, t, S64_K, max_first(wd, S64_K), px, py, pz, wd, wj);
     if (slow_ob) exact_select<MSL, true>(obst, M, -1, S64_MS, max_first(od, S64_MS), px, py, pz, od, oj);
   };
