@@ -201,6 +201,27 @@ __device__ __forceinline__ void kins(uint32_t (&k)[S], uint32_t key) {
   k[0] = min(k[0], key);
 }
 
+// kins into a list whose slots `filled` .. S-1 still hold KEY_EMPTY (`filled` must fold to a
+// constant): those slots stay empty, slot `filled` takes max(k[filled-1], key) — the med3 / min
+// against KEY_EMPTY that kins would issue are skipped (same list, fewer instructions).
+template <int S>
+__device__ __forceinline__ void kins_n(uint32_t (&k)[S], uint32_t key, int filled) {
+  if (filled >= S) {
+    kins<S>(k, key);
+    return;
+  }
+  if (filled == 0) {
+    k[0] = key;
+    return;
+  }
+#pragma unroll
+  for (int s = S - 1; s > 0; --s) {
+    if (s == filled) k[s] = max(k[s - 1], key);
+    else if (s < filled) k[s] = med3u(k[s - 1], key, k[s]);
+  }
+  k[0] = min(k[0], key);
+}
+
 // ------------------------------------------------------------------ Philox4x32-10 (device reset)
 __device__ __forceinline__ void philox4x32_10(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
@@ -1371,7 +1392,8 @@ union S64Lds {
 // arithmetic per element is sqsum_rank's (fma(z,z, fma(y,y, x*x)) of the same differences).
 typedef float s64_f2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(3))) float s64_lds_cf;
-template <int KS, int PASS, bool FAST, int RT, int NB, bool MIRROR>
+// F0: key slots filled before this group (the list starts empty at the pass's first group)
+template <int KS, int PASS, bool FAST, int RT, int NB, bool MIRROR, int F0 = (KS > 0 ? KS : 1)>
 __device__ __forceinline__ void pair_group_s64(s64_lds_cf* __restrict__ s0, uint32_t t4, float px, float py, float pz,
                                                bool self, uint32_t sflag, uint32_t keep, uint32_t keep_m, float ds,
                                                uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum,
@@ -1419,7 +1441,7 @@ __device__ __forceinline__ void pair_group_s64(s64_lds_cf* __restrict__ s0, uint
     for (int i = 0; i < NB; ++i) {
       if constexpr (KS > 0) {
         v[i] = (__float_as_uint(dv[i]) & keep) | (uint32_t)(RT - i);
-        kins<KS>(nk, v[i]);
+        kins_n<KS>(nk, v[i], F0 + i);
       } else {
         v[i] = __float_as_uint(dv[i]);
         smin = fminf(smin, dv[i]);  // no keys: the running minimum decides pair collisions
@@ -1431,7 +1453,7 @@ __device__ __forceinline__ void pair_group_s64(s64_lds_cf* __restrict__ s0, uint
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       v[i] = (__float_as_uint(pair_value<PASS>(sq[i])) & keep) | (uint32_t)(RT - i);
-      kins<KS>(nk, v[i]);
+      kins_n<KS>(nk, v[i], F0 + i);
     }
   } else {
 #pragma unroll
@@ -1449,7 +1471,7 @@ __device__ __forceinline__ void pair_group_s64(s64_lds_cf* __restrict__ s0, uint
         // the sender's key with its offset code RT - i swapped for the mirror's 64 - RT + i: one
         // v_xor_b32 (full rate) instead of v_and_or_b32 on the raw value (same key: the value
         // is >= 0, so keep and keep_m agree on it)
-        kins<KS>(nk, rc[i] ^ ((uint32_t)(RT - i) ^ (uint32_t)(64 - RT + i)));
+        kins_n<KS>(nk, rc[i] ^ ((uint32_t)(RT - i) ^ (uint32_t)(64 - RT + i)), F0 + NB + i);
       } else {
         mirror_pair<KS, PASS, FAST, false>(nk, rc[i], (uint32_t)(64 - RT + i), self, keep_m, ds, smin, esum);
       }
@@ -1461,17 +1483,18 @@ __device__ __forceinline__ void pair_group_s64(s64_lds_cf* __restrict__ s0, uint
   }
   if constexpr (PASS == 1) fsum += (double)esum;
 }
-template <int KS, int PASS, bool FAST, int RT, int B>
+template <int KS, int PASS, bool FAST, int RT, int B, int F0 = (KS > 0 ? KS : 1)>
 __device__ __forceinline__ void pair_groups_s64(s64_lds_cf* __restrict__ s0, uint32_t t4, float px, float py, float pz,
                                                 bool self, uint32_t sflag, uint32_t keep, uint32_t keep_m, float ds,
                                                 uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum,
                                                 float& macc) {
   if constexpr (RT >= 1) {
     constexpr int NB = RT < B ? RT : B;
-    pair_group_s64<KS, PASS, FAST, RT, NB, true>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum,
-                                                 macc);
-    pair_groups_s64<KS, PASS, FAST, RT - NB, B>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum,
-                                                macc);
+    constexpr int F1 = F0 + 2 * NB < KS ? F0 + 2 * NB : (KS > 0 ? KS : 1);
+    pair_group_s64<KS, PASS, FAST, RT, NB, true, F0>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum,
+                                                     macc);
+    pair_groups_s64<KS, PASS, FAST, RT - NB, B, F1>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin,
+                                                    fsum, macc);
   }
 }
 // `soa` = the wave's pair-pass ring (S64Lds::soa); lane t reads from soa + t.
@@ -1488,8 +1511,9 @@ __device__ __forceinline__ void pair_pass_s64(const float* __restrict__ soa, int
   s64_lds_cf* s0 = (s64_lds_cf*)(soa + t);
   asm volatile("" : "+v"(s0));
   float macc = 0.f;
-  pair_groups_s64<KS, PASS, FAST, 31, SWARM_PAIR_BATCH>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk,
-                                                        smin, fsum, macc);
+  // every caller starts the pass with an empty key list (F0 = 0)
+  pair_groups_s64<KS, PASS, FAST, 31, SWARM_PAIR_BATCH, 0>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk,
+                                                           smin, fsum, macc);
   if constexpr (PASS == 1) fsum += (double)wave_ror1(macc);
   // rotation 32 pairs t with t+32 from both sides: own evaluation only
   pair_group_s64<KS, PASS, FAST, 32, 1, false>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum,
@@ -1508,7 +1532,9 @@ __device__ __forceinline__ void obstacle_pass_s64(const float* __restrict__ os, 
   s64_f2 X = {os[0], os[1]};
   s64_f2 Y = {os[S64_MMAX], os[S64_MMAX + 1]};
   s64_f2 Z = {os[2 * S64_MMAX], os[2 * S64_MMAX + 1]};
-  for (; m + 1 < M; m += 2) {
+  // `filled`: key slots filled before pair m (the list starts empty; the first two pairs are
+  // peeled, M >= 4 for every caller: Ms = 4 <= M)
+  auto pair = [&](int filled) {
     const int n = m + 2 < S64_MMAX - 1 ? m + 2 : S64_MMAX - 2;
     const s64_f2 Xn = {os[n], os[n + 1]};
     const s64_f2 Yn = {os[S64_MMAX + n], os[S64_MMAX + n + 1]};
@@ -1519,11 +1545,15 @@ __device__ __forceinline__ void obstacle_pass_s64(const float* __restrict__ os, 
     Z = Zn;
     const s64_f2 sq = (dx * dx + dy * dy) + dz * dz;
     if constexpr (MSL > 0) {
-      kins<MSL>(ok, (__float_as_uint(sq.x) & keep) | (uint32_t)m);
-      kins<MSL>(ok, (__float_as_uint(sq.y) & keep) | (uint32_t)(m + 1));
+      kins_n<MSL>(ok, (__float_as_uint(sq.x) & keep) | (uint32_t)m, filled);
+      kins_n<MSL>(ok, (__float_as_uint(sq.y) & keep) | (uint32_t)(m + 1), filled + 1);
     }
     if constexpr (COLL) coll = coll || (chk && ((sq.x <= s_thr) || (sq.y <= s_thr)));
-  }
+  };
+  pair(0);
+  m = 2;
+  pair(2);
+  for (m = 4; m + 1 < M; m += 2) pair(MSL > 0 ? MSL : 1);
   if (m < M) {
     const float sq = sqsum_f(os[m] - px, os[S64_MMAX + m] - py, os[2 * S64_MMAX + m] - pz);
     if constexpr (MSL > 0) kins<MSL>(ok, (__float_as_uint(sq) & keep) | (uint32_t)m);
