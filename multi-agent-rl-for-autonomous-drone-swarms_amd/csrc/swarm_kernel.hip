@@ -2534,7 +2534,8 @@ __device__ __forceinline__ void q16_pair_pass(const float* __restrict__ soa, int
     const float s = sqsum_rank(soa[j] - px, soa[32 + j] - py, soa[64 + j] - pz);
     const float v = PASS == 1 ? __builtin_amdgcn_sqrtf(s) : s;
     const bool el = FAST || (self && soa[96 + j] != 0.f);
-    kins<4>(nk, (__float_as_uint(v) & keep) | (uint32_t)r);
+    // the list starts empty: inserts 1 .. 4 of the pass skip the compares against KEY_EMPTY
+    kins_n<4>(nk, (__float_as_uint(v) & keep) | (uint32_t)r, 2 * it);
     if constexpr (PASS == 1) {
       if constexpr (!FAST) smin = fminf(smin, el ? v : __builtin_inff());
       esum += el ? fabsf(v - ds) : 0.f;
@@ -2545,7 +2546,7 @@ __device__ __forceinline__ void q16_pair_pass(const float* __restrict__ soa, int
     if (r < 8) {
       const float vm = __uint_as_float(rcv & 0x7fffffffu);
       const bool pr = FAST || (self && !(rcv >> 31));
-      kins<4>(nk, (rcv & keep_m) | (uint32_t)(Q_N - r));
+      kins_n<4>(nk, (rcv & keep_m) | (uint32_t)(Q_N - r), 2 * it + 1);
       if constexpr (PASS == 1) {
         if constexpr (!FAST) smin = fminf(smin, pr ? vm : __builtin_inff());
         esum += pr ? fabsf(vm - ds) : 0.f;
