@@ -596,11 +596,18 @@ def main(argv=None):
     ev_all = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     streams_g = vec.group_streams if G > 1 else [stream]
 
+    raw_launch = native_groups  # plain steps: launch group g straight onto its stream handle
+
     def body_eager():
         ev_all[0].record(stream)
         fork(ev_all[0])
         for k in range(args.steps):
             for g, st in enumerate(streams_g):
+                if raw_launch:
+                    ev[g][k][0].record(st)
+                    vec._launch_step(g, ring[k % args.ring], None, vec._gstream_h[g])
+                    ev[g][k][1].record(st)
+                    continue
                 with torch.cuda.stream(st):
                     ev[g][k][0].record(st)
                     env_step_group(g, k)
@@ -642,12 +649,17 @@ def main(argv=None):
                                    f"measured in this run") if prof else None,
                 "algorithmic_bytes_per_launch": bytes_launch,
                 "kernel_ms_mean": kern_max,
-                "kernel_ms_timing": ("HIP events on the launch stream around the timed region "
-                                     "(graph replays), / K; max over ranks") if G == 1 else
+                "kernel_ms_timing": (f"HIP events on the launch stream around the timed region "
+                                     f"({'graph replays' if use_graph else 'eager launches'}), / K; max over ranks")
+                                    if G == 1 else
+                                    (f"HIP events on every group stream around the timed region (eager "
+                                     f"launches): last end - first start, / K = whole-batch step time "
+                                     f"({G} overlapping launches of E/{G} envs per step); max over ranks")
+                                    if not use_graph and free else
                                     (f"HIP events on the launch stream around the timed region, "
-                                     f"forked to and joined from the {G} group streams (graph "
-                                     f"replays), / K = whole-batch step time ({G} overlapping "
-                                     f"launches of E/{G} envs per step); max over ranks"),
+                                     f"forked to and joined from the {G} group streams ("
+                                     f"{'graph replays' if use_graph else 'eager launches'}), / K = whole-batch "
+                                     f"step time ({G} overlapping launches of E/{G} envs per step); max over ranks"),
                 "kernel_ms_eager_events": kern_eager_max,
                 "kernel_ms_per_launch": launch_max,
                 "kernel_ms_per_launch_timing": "eager pass, HIP events around each launch on its own "
