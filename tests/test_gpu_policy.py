@@ -52,8 +52,13 @@ def test_bf16_logits_vs_emulation_and_graph(dev, fx):
     pol = _pol(fx, dev, "bf16")
     got = pol.logits(torch.as_tensor(d["obs"]).to(dev)).cpu().numpy()
     emu = emulate_bf16_kernel(pol.packed_host, d["obs"], 6)
-    assert np.abs(got - emu).max() <= 0.02, np.abs(got - emu).max()
-    assert np.abs(got - d["logits"]).max() <= 0.3
+    # the kernel against a host emulation of its own bf16 arithmetic (operand roundings, f32 sums):
+    # measured 1.8e-4 (tools/policy_err.py), bound 1e-3
+    assert np.abs(got - emu).max() <= 1e-3, np.abs(got - emu).max()
+    # against the reference's f32 graph the bf16 operand rounding (2^-9 relative) shows: measured
+    # 0.225 max / 0.018 mean on logits up to |66| (0.34 % of the range); bounds 0.3 / 0.03
+    err = np.abs(got - d["logits"])
+    assert err.max() <= 0.3 and err.mean() <= 0.03, (err.max(), err.mean())
 
 
 @pytest.mark.parametrize("precision", ["bf16", "f32"])
