@@ -49,7 +49,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # (16 lanes/clk) x 1024 SIMDs x 2.4 GHz.  The 157.3 TFLOP/s f32 spec counts a packed FMA as 4
 # FLOPs per lane (MI355X_MICROARCH.md: 64 FLOP/clk/SIMD); SQ_INSTS_VALU x 64 counts instruction-lanes.
 VALU_PEAK_LANE_OPS = 39.3e12
-MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA peaks, MI355X_MICROARCH.md
+# dense MFMA peaks, MI355X_MICROARCH.md; f32x3 runs three f16 MFMA passes per f32 product, so the
+# f32-graph FLOPs it can deliver peak at a third of the f16 (= bf16) rate
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3, "f32x3": 2500.0 / 3}
 
 # BASELINE.json configs, per GPU: [2] is the headline (the metric's config), [1] and [4] have
 # their own bench lines (profiles/r02_config_lines.jsonl).
@@ -89,10 +91,12 @@ def parse(argv=None):
                     help="time the whole-job rate with eager launches instead of hipGraph replay")
     ap.add_argument("--ctde", action="store_true", default=None,
                     help="also emit global_state and all-gather it (config 5)")
+    ap.add_argument("--no-ctde", dest="ctde", action="store_false",
+                    help="no global_state output (the n256 preset emits it by default)")
     ap.add_argument("--eval", action="store_true",
                     help="on-device eval metrics every step (EvalTracker: swarm_eval_update per env group "
                          "after its step; the envs carry infos): the evaluation-protocol rollout")
-    ap.add_argument("--policy", choices=("bf16", "f32"), default=None,
+    ap.add_argument("--policy", choices=("bf16", "f32", "f32x3"), default=None,
                     help="rollout mode: each step = on-device actor inference on the obs tensor "
                          "(swarm_policy_forward, random-init TorchFC 256x256 weights) + the env step")
     ap.add_argument("--device-warmup-ms", type=float, default=200.0,
@@ -142,8 +146,9 @@ def parse(argv=None):
         # 26.7 us (headline), 56.2 vs 61.0 us (n256); eager short regions (the driver's K = 20)
         # keep 2 — four streams' eager launches cost the host ~20 us per step and measured
         # 44-52 us (profiles/r03_groups_ab.jsonl)
-        gathering = a.ctde and int(os.environ.get("WORLD_SIZE", "1")) > 1
-        graph_long = a.steps > 256 and not a.no_graph and not gathering
+        gathering = a.ctde and (int(os.environ.get("WORLD_SIZE", "1")) > 1
+                                or os.environ.get("SWARM_BENCH_FORCE_GATHER") == "1")
+        graph_long = a.steps > 256 and not a.no_graph and not gathering and not a.eval
         a.groups = pre.get("groups_graph", pre.get("groups", 1)) if graph_long else pre.get("groups", 1)
     if a.groups < 1:
         ap.error("--groups must be >= 1")
@@ -304,6 +309,15 @@ def main(argv=None):
         dist.init_process_group("gloo" if rehearsal else "nccl")
     dev = torch.device("cuda", local if world > 1 and not rehearsal else 0)
     torch.cuda.set_device(dev)
+    own_pg = False
+    if world == 1 and os.environ.get("SWARM_BENCH_FORCE_GATHER") == "1" and args.ctde and not dist.is_initialized():
+        # the CTDE gather on one GPU: a one-rank RCCL group (its cost on the step)
+        import socket
+        with socket.socket() as so_:
+            so_.bind(("127.0.0.1", 0))
+            port = so_.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        own_pg = True
 
     from swarm_marl_amd import VecSwarm
 
@@ -417,7 +431,7 @@ def main(argv=None):
         if G > 1:
             for st in vec.group_streams[1:]:
                 stream.wait_stream(st)
-        if gatherer is not None:  # the timed region ends after the last gather
+        if gatherer is not None and gatherer.stream is not None:  # the region ends after the last gather
             stream.wait_stream(gatherer.stream)
 
     # ---- timed region: hipGraph replay of ring segments (or eager with --no-graph / CTDE)
@@ -428,7 +442,10 @@ def main(argv=None):
     # short timed regions (the driver's K = 20) launch eagerly: a replayed graph's kernels ran
     # slower there (27.5-28.8 vs 30.8-32.3 us per step by events, tools/r03x_cmd.sh); graphs for
     # long regions, where the host's ~5 us per launch would otherwise matter
-    use_graph = not args.no_graph and gatherer is None and (args.steps > 256 or args.graph_short)
+    # --eval launches eagerly: a captured swarm_eval_update would replay its capture-time update
+    # index, so the records' update order and the update count would be wrong
+    use_graph = (not args.no_graph and gatherer is None and tracker is None
+                 and (args.steps > 256 or args.graph_short))
     reps, rem = divmod(args.steps, args.ring)
     if use_graph:
         def capture(n_steps, k0=0):  # one graph of n_steps ring steps per group, on its group stream
@@ -540,7 +557,7 @@ def main(argv=None):
                 join()
                 t_ev[1].record(stream)
         timing = "eager launches" + (f", {G} env groups on {G} HIP streams" if G > 1 else "") + (
-            f", CTDE all-gather every {args.gather_every} steps on a side stream ({args.gs_slots}-slot "
+            f", CTDE all-gather every {args.gather_every} steps from the default stream when no group launches there, else a side stream ({args.gs_slots}-slot "
             f"global_state ring{', gloo host-staged' if gatherer is not None and gatherer.staged else ''})"
             if gatherer is not None else "")
     # every event the region records exists before it: torch creates an event's HIP object at
@@ -735,7 +752,7 @@ def main(argv=None):
             if args.cpu_variant_seconds > 0 and not args.no_term and args.dynamics == "kinematic":
                 rec["cpu_baseline_variants"] = cpu_python_variants(n, e, args.cpu_variant_seconds)
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if world > 1 or own_pg:
         dist.destroy_process_group()
 
 

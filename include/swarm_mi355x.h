@@ -279,13 +279,18 @@ int swarm_observe(const swarm_params_t* p, const swarm_state_t* s, const uint8_t
 #define SWARM_POLICY_MAX_OUT 12     /* logits (2 x action dim) */
 #define SWARM_POLICY_BF16 0         /* v_mfma_f32_32x32x16_bf16: bf16 operands, f32 accumulation */
 #define SWARM_POLICY_F32 1          /* v_mfma_f32_16x16x4_f32: f32 operands and sums */
+#define SWARM_POLICY_F32X3 2        /* v_mfma_f32_32x32x16_f16, three passes: every f32 operand split
+                                       into f16 hi + lo, products hi*hi + hi*lo + lo*hi (~2^-21
+                                       relative per product: the f32 path's tolerance at f16-MFMA
+                                       speed); obs, weights and activations must be < 65504 in
+                                       magnitude (f16 range) */
 #define SWARM_POLICY_ACT_MEAN 0     /* actions = mean (deterministic) */
 #define SWARM_POLICY_ACT_SAMPLE 1   /* actions = mean + exp(log_std) * N(0,1), Philox(seed; row, counter) */
 
 typedef struct swarm_policy {
   int32_t in_dim;        /* observation width D */
   int32_t out_dim;       /* logits width (even) */
-  int32_t precision;     /* SWARM_POLICY_BF16 / SWARM_POLICY_F32 */
+  int32_t precision;     /* SWARM_POLICY_BF16 / SWARM_POLICY_F32 / SWARM_POLICY_F32X3 */
   int32_t reserved;
   const void* weights;   /* device copy of the swarm_policy_pack blob (16-B aligned) */
 } swarm_policy_t;

@@ -2446,11 +2446,16 @@ constexpr int Q_MMAX = 16;
 constexpr uint64_t Q_LEAD = 0x1111111111111111ull;  // quarter 0 of every drone
 constexpr int Q_WG_ENVS = 4;                        // independent one-env waves per workgroup
 
-struct Q16Lds {
-  float soa[4 * 32];  // x, y, z, eligibility planes; drone j at j and j + 16
-  float4 ring[Q_N];
-  float4 obst[Q_MMAX];
-  float osoa[3 * Q_MMAX];
+union Q16Lds {
+  struct {
+    float soa[4 * 32];  // x, y, z, eligibility planes; drone j at j and j + 16
+    float4 ring[Q_N];
+    float4 obst[Q_MMAX];
+    float osoa[3 * Q_MMAX];
+  };
+  // the env's 16 obs rows (2,368 B), staged once the rows are in registers: the block leaves as
+  // 148 aligned 16-B stores (whole 128-B lines) instead of 8-13 scattered dword stores per lane
+  float4 stage[Q_N * Q_D / 4];
 };
 
 // DPP quad permutations: xor 1, xor 2, broadcast of quad lane k
@@ -2573,6 +2578,12 @@ __device__ __forceinline__ void q16_pair_pass(const float* __restrict__ soa, int
 #ifndef SWARM_LAT_REFETCH_ON
 #define SWARM_LAT_REFETCH_ON 0
 #endif
+#ifndef SWARM_Q16_DIRECT_OBS
+#define SWARM_Q16_DIRECT_OBS 0
+#endif
+#ifndef SWARM_Q16_FLOOR
+#define SWARM_Q16_FLOOR 0
+#endif
 #define SWARM_LAT_REFETCH(A) \
   do {                       \
     if (SWARM_LAT_REFETCH_ON) (A) = s64_args(); \
@@ -2625,6 +2636,40 @@ swarm_step16q(const S64Args args) {
   const int n_active = __popcll(__ballot(act) & Q_LEAD);
   STAMP_AT(env, 1);
   SWARM_LAT_REFETCH(A);
+#if SWARM_Q16_FLOOR
+  {  // diagnostic bytes-only floor (tools: the achievable time of a one-wave-per-SIMD launch that
+     // moves this step's bytes): every input read above, every output written below in the
+     // product's store pattern, no pair / obstacle / reward / reset / finish work (wrong values)
+    const float f = ax + ay + az + gx + gy + gz + (float)stepc + (float)episode0 + (float)n_active;
+    if (q == 0) {
+      A->O.reward[ag] = f;
+      float* pe = A->S.pos + ag * 3;
+      float* ve = A->S.vel + ag * 3;
+      pe[0] = px; pe[1] = py; pe[2] = pz;
+      ve[0] = vx + f; ve[1] = vy; ve[2] = vz;
+    }
+    if (lane == 0) { A->O.env_done[env] = (uint8_t)f; A->S.step_count[env] = stepc + 1; }
+    const uint64_t m = __ballot(act && has);
+    if ((lane >> 2) < 3) {
+      uint8_t* base = (lane >> 2) == 0 ? A->O.terminated : ((lane >> 2) == 1 ? A->O.truncated : A->S.active);
+      *reinterpret_cast<uint32_t*>(base + ea + 4 * (lane & 3)) = (uint32_t)(m >> (16 * (lane & 3)));
+    }
+    wave_sync();
+    float* row = reinterpret_cast<float*>(L.stage) + d * Q_D;
+#pragma unroll
+    for (int c = 0; c < 9; ++c) row[q * 9 + c] = px + (float)c;
+    if (q == 0) row[36] = py;
+    wave_sync();
+    constexpr int V4 = Q_N * Q_D / 4;
+    const float4 v0 = L.stage[lane], v1 = L.stage[lane + 64];
+    const float4 v2 = L.stage[lane + 128 < V4 ? lane + 128 : V4 - 1];
+    float* ob = A->O.obs + ea * Q_D;
+    store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)lane, v0);
+    store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)(lane + 64), v1);
+    if (lane + 128 < V4) store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)(lane + 128), v2);
+    return;
+  }
+#endif
 
   // ---- integrate: drone_swarm_env.py:98-117 (swarm_kernel, DYN_KIN)
   float prev_d = 0.f;
@@ -2905,8 +2950,14 @@ swarm_step16q(const S64Args args) {
   STAMP_AT(env, 7);
   SWARM_LAT_REFETCH(A);
 
-  // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)], straight from registers
+  // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)]: the lanes' pieces into
+  // the LDS stage (aliasing the dead rings), then the env's block as coalesced 16-B stores
+#if SWARM_Q16_DIRECT_OBS  // diagnostic: round 3's scattered dword stores straight from registers
   float* row = A->O.obs + ag * Q_D;
+#else
+  wave_sync();  // every ring / obstacle read of the finish is issued before the stage overwrites them
+  float* row = reinterpret_cast<float*>(L.stage) + d * Q_D;
+#endif
   if (q < 3) {
     row[9 + 4 * q] = ndx; row[10 + 4 * q] = ndy; row[11 + 4 * q] = ndz; row[12 + 4 * q] = nd;
   } else {
@@ -2915,6 +2966,18 @@ swarm_step16q(const S64Args args) {
     row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
   }
   row[21 + 4 * q] = odx; row[22 + 4 * q] = ody; row[23 + 4 * q] = odz; row[24 + 4 * q] = od;
+#if !SWARM_Q16_DIRECT_OBS
+  wave_sync();
+  {
+    constexpr int V4 = Q_N * Q_D / 4;  // 148 float4: lanes take 64 + 64 + 20
+    const float4 v0 = L.stage[lane], v1 = L.stage[lane + 64];
+    const float4 v2 = L.stage[lane + 128 < V4 ? lane + 128 : V4 - 1];
+    float* ob = A->O.obs + ea * Q_D;  // 16-B aligned: 2,368 B per env
+    store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)lane, v0);
+    store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)(lane + 64), v1);
+    if (lane + 128 < V4) store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)(lane + 128), v2);
+  }
+#endif
   STAMP_AT(env, 8);
 #ifdef SWARM_STAMPS
   if (lane == 0 && env < (1 << 16)) g_stamps[env * 16 + 12] = __builtin_amdgcn_s_memrealtime();
@@ -3831,7 +3894,7 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
     if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SWARM_OK;
   }
-  if (mode == MODE_STEP && step16q_applies(p, kp) && !s->env_cfg &&
+  if (mode == MODE_STEP && step16q_applies(p, kp) && !s->env_cfg && ((uintptr_t)o->obs) % 16 == 0 &&
       ((uintptr_t)o->terminated | (uintptr_t)o->truncated | (uintptr_t)s->active) % 4 == 0) {
     const S64Args args{kp, *s, actions, amask, *o};
     hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step16q()), dim3((kp.E + Q_WG_ENVS - 1) / Q_WG_ENVS),

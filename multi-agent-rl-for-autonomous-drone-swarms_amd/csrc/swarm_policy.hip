@@ -79,6 +79,41 @@ __host__ __device__ inline int chained_k(int ks, int h, int j) {
 // f32 16x16x4 chaining: k-step q (of 64) of lane quarter g -> hidden unit
 __host__ __device__ inline int chained_k_f32(int q, int g) { return (q >> 2) * 16 + 4 * g + (q & 3); }
 
+// IEEE binary16, round to nearest even (subnormals kept; overflow -> inf); and back
+uint16_t f16_rne(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  const uint32_t sign = (u >> 16) & 0x8000u;
+  const uint32_t a = u & 0x7fffffffu;
+  if (a >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (a > 0x7f800000u ? 0x200u : 0u));
+  if (a >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);  // rounds past 65504
+  if (a < 0x38800000u) {  // f16 subnormal (or zero): value / 2^-24, rounded to nearest even
+    if (a < 0x33000000u) return (uint16_t)sign;  // below half the smallest subnormal
+    const uint32_t e = a >> 23, mant = (a & 0x7fffffu) | 0x800000u;
+    const int shift = 126 - (int)e;  // mant * 2^(e-150) / 2^-24 = mant >> (126 - e)
+    uint32_t q = mant >> shift;
+    const uint32_t rem = mant & ((1u << shift) - 1u), half = 1u << (shift - 1);
+    if (rem > half || (rem == half && (q & 1u))) ++q;
+    return (uint16_t)(sign | q);
+  }
+  uint32_t r = a - 0x38000000u;  // rebias 127 -> 15
+  const uint32_t lsb = (r >> 13) & 1u;
+  r += 0xfffu + lsb;
+  return (uint16_t)(sign | (r >> 13));
+}
+float f16_to_f32(uint16_t h) {
+  const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+  const uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+  float f;
+  if (e == 0) {
+    f = (float)m * 0x1p-24f;
+    return sign ? -f : f;
+  }
+  uint32_t u = e == 31 ? (sign | 0x7f800000u | (m << 13)) : (sign | ((e + 112u) << 23) | (m << 13));
+  memcpy(&f, &u, 4);
+  return f;
+}
+
 uint16_t bf16_rne(float f) {
   uint32_t u;
   memcpy(&u, &f, 4);
@@ -410,6 +445,230 @@ __global__ void __launch_bounds__(64 * WAVES) policy_mlp_f32(const FwdArgs A) {
   }
 }
 
+// ---------------------------------------------------------------- f32x3 kernel (split f16, three passes)
+// The f32 graph at f16-MFMA speed (SWARM_POLICY_F32X3): every f32 operand v is split into
+// hi = f16(v) and lo = f16((v - hi) * 2^11) (v - hi is exact in f32 and at most half an f16 ulp,
+// 2^-11 |v|, so the scaled lo stays in the f16 normal range down to |v| ~ 6e-5 and keeps 11
+// bits: |v - hi - lo 2^-11| <= 2^-22 |v|).  Every product is hi*hi into one f32 accumulator and
+// hi*lo + lo*hi into a second (both scaled by 2^11) on v_mfma_f32_32x32x16_f16; the layer output
+// is acc_hh + 2^-11 acc_x.  The dropped lo*lo term is <= 2^-22 relative, so each product carries
+// ~2^-21 relative error against f32's 2^-24 and the layer sums stay within the f32 path's
+// tolerance.  (Unscaled, lo of a weight below ~0.1 is an f16 subnormal and loses bits.)
+// Structure of policy_mlp_bf16 (T = 1): transposed layers, accumulators split in place into the
+// next layer's hi / lo B fragments; W hi in LDS (the bf16 blob's fragment order, f16 elements),
+// W lo streamed from global memory (L1 / L2-resident: every wave of a workgroup reads the same
+// fragments in the same order) by buffer loads with SGPR offsets.
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
+typedef int v4i __attribute__((ext_vector_type(4)));
+constexpr float X3_LO_SCALE = 2048.f, X3_LO_INV = 1.f / 2048.f;
+#ifndef SWARM_POLICY_X3_BATCH
+#define SWARM_POLICY_X3_BATCH 8
+#endif
+constexpr int X3_B = SWARM_POLICY_X3_BATCH;  // W2 k-steps per lo-fragment batch (divides 16)
+
+// 8 accumulator values (sub-block s) -> hi / lo f16 fragments, relu'd first when `act`
+__device__ __forceinline__ void split8(const f32x16& a, int s, bool act, f16x8& hi, f16x8& lo) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float x0 = a[8 * s + 2 * q], x1 = a[8 * s + 2 * q + 1];
+    if (act) {
+      x0 = x0 > 0.f ? x0 : 0.f;
+      x1 = x1 > 0.f ? x1 : 0.f;
+    }
+    const f16x2 h = __builtin_convertvector((f32x2){x0, x1}, f16x2);
+    const f32x2 hb = __builtin_convertvector(h, f32x2);
+    const f16x2 l = __builtin_convertvector((f32x2){(x0 - hb.x) * X3_LO_SCALE, (x1 - hb.y) * X3_LO_SCALE}, f16x2);
+    hi[2 * q] = h.x; hi[2 * q + 1] = h.y;
+    lo[2 * q] = l.x; lo[2 * q + 1] = l.y;
+  }
+}
+__device__ __forceinline__ f16x8 wlo_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
+}
+// hi*hi into c, the cross terms (scaled by 2^11) into x (hi*lo) and y (lo*hi): three
+// independent accumulator chains, so one wave per SIMD issues the three MFMAs of a k-step back to
+// back without waiting for a dependent result
+__device__ __forceinline__ void mfma3(const f16x8& ah, const f16x8& al, const f16x8& bh, const f16x8& bl, f32x16& c,
+                                      f32x16& x, f32x16& y) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
+  x = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, x, 0, 0, 0);
+  y = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, y, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 x3_sum(const f32x16& c, const f32x16& x, const f32x16& y) {
+  f32x16 r;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) r[i] = c[i] + (x[i] + y[i]) * X3_LO_INV;
+  return r;
+}
+
+template <int WAVES, int IN_C = 0, int OUT_C = 0>
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVES / 4 > 0 ? WAVES / 4 : 1)))
+policy_mlp_x3(const FwdArgs A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const Bf16Layout L(A.out);
+  {  // stage the hi blob (f16 fragments + f32 biases, ~159 KB) in LDS, once per workgroup
+    const int4* src = reinterpret_cast<const int4*>(A.w);
+    int4* dst = reinterpret_cast<int4*>(lds);
+    const int n16 = (int)(L.total / 16);
+    constexpr int UNR = 8, STRIDE = 64 * WAVES;
+    for (int base = threadIdx.x; base < n16; base += STRIDE * UNR) {
+      int4 v[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int i = base + u * STRIDE;
+        v[u] = src[i < n16 ? i : n16 - 1];
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int i = base + u * STRIDE;
+        if (i < n16) dst[i] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  // the lo blob: right after the hi blob
+  const __amdgpu_buffer_rsrc_t WL = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char*>(reinterpret_cast<const unsigned char*>(A.w) + L.total), 0, (int)L.total, BUF_DWORD3);
+  const int wave = threadIdx.x >> 6;
+  const long long ntiles = (A.rows + 31) / 32;
+  const float* b2 = reinterpret_cast<const float*>(lds + L.b2);
+  const float* b3 = reinterpret_cast<const float*>(lds + L.b3);
+  for (long long tile = (long long)blockIdx.x * WAVES + wave; tile < ntiles; tile += (long long)gridDim.x * WAVES) {
+    int lane = threadIdx.x & 63, in_r = A.in, out_r = A.out;
+    uint32_t sb = 0;
+    asm volatile("" : "+v"(lane), "+s"(in_r), "+s"(out_r), "+s"(sb));
+    const int in = IN_C ? IN_C : in_r, out = OUT_C ? OUT_C : out_r;
+    const int n = lane & 31, h = (lane >> 5) & 1;
+    const bool w3lane = n < out;
+    const int w3idx = h * out + n;
+    const uint32_t lb = 16u * (uint32_t)lane;
+    const f16x8* w1f = reinterpret_cast<const f16x8*>(lds + L.w1 + lb);
+    const f16x8* w2f = reinterpret_cast<const f16x8*>(lds + L.w2 + lb);
+    const f16x8* w3f = reinterpret_cast<const f16x8*>(lds + L.w3);
+    const long long row = tile * 32 + n;
+    const bool valid = row < A.rows;
+    // ---- obs fragments, split: x[row][16 ks + 8 h + j], x[in] = 1 (bias column)
+    f16x8 xh[KS1], xl[KS1];
+    {
+      const float* xr = A.obs + (valid ? row : A.rows - 1) * in;
+      float xv[KS1 * 8];
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 16 * ks + 8 * h + j;
+          xv[ks * 8 + j] = xr[k < in ? k : in - 1];
+        }
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const int k0 = 16 * ks + 8 * h + j, k1 = k0 + 1;
+          const float x0 = k0 < in ? xv[ks * 8 + j] : (k0 == in ? 1.f : 0.f);
+          const float x1 = k1 < in ? xv[ks * 8 + j + 1] : (k1 == in ? 1.f : 0.f);
+          const f16x2 hh = __builtin_convertvector((f32x2){x0, x1}, f16x2);
+          const f32x2 hb = __builtin_convertvector(hh, f32x2);
+          const f16x2 ll = __builtin_convertvector((f32x2){(x0 - hb.x) * X3_LO_SCALE, (x1 - hb.y) * X3_LO_SCALE}, f16x2);
+          xh[ks][j] = hh.x; xh[ks][j + 1] = hh.y;
+          xl[ks][j] = ll.x; xl[ks][j + 1] = ll.y;
+        }
+    }
+    // ---- layer 1: 256 x (in + 1), relu -> h1 hi / lo (16 k-step fragments each)
+    f16x8 h1h[KS2], h1l[KS2];
+#pragma unroll
+    for (int ob = 0; ob < OB; ++ob) {
+      f32x16 acc = f32x16{}, accx = f32x16{}, accy = f32x16{};
+      f16x8 w1l[KS1];
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks) w1l[ks] = wlo_load(WL, lb, sb + (uint32_t)(L.w1 + (size_t)(ob * KS1 + ks) * FRAG));
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks)
+        mfma3(w1f[(ob * KS1 + ks) * 64], w1l[ks], xh[ks], xl[ks], acc, accx, accy);
+      acc = x3_sum(acc, accx, accy);
+      split8(acc, 0, true, h1h[2 * ob], h1l[2 * ob]);
+      split8(acc, 1, true, h1h[2 * ob + 1], h1l[2 * ob + 1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- layer 2 (relu) fused with layer 3: each out block's two split fragments feed layer 3's
+    // k-steps 2ob, 2ob+1 at once
+    f32x16 acc3, acc3x = f32x16{}, acc3y = f32x16{};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
+      acc3[i] = m < out ? b3[m] : 0.f;
+    }
+    // W2 lo fragments stream in batches of X3_B k-steps, double-buffered: batch b + 1's loads are
+    // issued before batch b's MFMAs (128 fragments per wave in (ob, ks) order)
+    constexpr int NB2 = OB * KS2 / X3_B;
+    f16x8 wlb[2][X3_B];
+#pragma unroll
+    for (int u = 0; u < X3_B; ++u) wlb[0][u] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)u * FRAG));
+#pragma unroll
+    for (int ob = 0; ob < OB; ++ob) {
+      f32x16 acc, accx = f32x16{}, accy = f32x16{};
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 b = *reinterpret_cast<const float4*>(b2 + ob * 32 + 8 * g + 4 * h);
+        acc[4 * g + 0] = b.x; acc[4 * g + 1] = b.y; acc[4 * g + 2] = b.z; acc[4 * g + 3] = b.w;
+      }
+#pragma unroll
+      for (int kb = 0; kb < KS2; kb += X3_B) {
+        const int bi = (ob * KS2 + kb) / X3_B;  // batch index
+        if (bi + 1 < NB2) {
+#pragma unroll
+          for (int u = 0; u < X3_B; ++u)
+            wlb[(bi + 1) & 1][u] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)((bi + 1) * X3_B + u) * FRAG));
+        }
+        f16x8 wh[X3_B];
+#pragma unroll
+        for (int u = 0; u < X3_B; ++u) wh[u] = w2f[(ob * KS2 + kb + u) * 64];
+#pragma unroll
+        for (int u = 0; u < X3_B; ++u) mfma3(wh[u], wlb[bi & 1][u], h1h[kb + u], h1l[kb + u], acc, accx, accy);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      acc = x3_sum(acc, accx, accy);
+      f16x8 a0h = {}, a1h = {}, a0l = {}, a1l = {};
+      if (w3lane) {
+        a0h = w3f[(2 * ob) * 2 * out + w3idx];
+        a1h = w3f[(2 * ob + 1) * 2 * out + w3idx];
+        a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob) * 2 * out * 16));
+        a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob + 1) * 2 * out * 16));
+      }
+      f16x8 h2h, h2l;
+      split8(acc, 0, true, h2h, h2l);
+      mfma3(a0h, a0l, h2h, h2l, acc3, acc3x, acc3y);
+      split8(acc, 1, true, h2h, h2l);
+      mfma3(a1h, a1l, h2h, h2l, acc3, acc3x, acc3y);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    acc3 = x3_sum(acc3, acc3x, acc3y);
+    // ---- outputs: lane holds logits m = (i&3) + 8(i>>2) + 4h of its row (out <= 12: i < 8)
+    if (A.logits && valid) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (m < out) A.logits[row * out + m] = acc3[i];
+      }
+    }
+    if (A.actions) {
+      float lg[12];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        lg[i] = acc3[i];
+        lg[4 + i] = __shfl_xor(acc3[i], 32);
+        lg[8 + i] = acc3[4 + i];
+      }
+      const int ad = out / 2;
+      if (h == 0 && valid) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+          if (k < ad) A.actions[row * ad + k] = lg[k];
+      }
+    }
+  }
+}
+
 #ifndef SWARM_POLICY_WAVES
 #define SWARM_POLICY_WAVES 8
 #endif
@@ -420,6 +679,13 @@ constexpr int BF16_WAVES = SWARM_POLICY_WAVES;  // T = 1: waves per workgroup (o
 constexpr int BF16_TILES = SWARM_POLICY_TILES;            // row tiles per wave
 constexpr int BF16_WAVES_T = BF16_TILES > 1 ? 4 : BF16_WAVES;  // T = 2: one wave per SIMD
 constexpr int F32_WAVES = 4;
+#ifndef SWARM_POLICY_X3_WAVES
+#define SWARM_POLICY_X3_WAVES 4
+#endif
+// f32x3: waves per workgroup (one workgroup per CU: the LDS blob); 4 = one wave per SIMD: the hi
+// and lo fragments of h1 (128 VGPRs), three accumulator chains and the double-buffered W2 lo
+// batches need ~330 registers (at 2 waves per SIMD, 256, it spills)
+constexpr int X3_WAVES = SWARM_POLICY_X3_WAVES;
 
 thread_local char g_perr[256] = "";
 int pfail(int code, const char* msg) {
@@ -450,6 +716,7 @@ long long swarm_policy_packed_bytes(int in_dim, int out_dim, int precision) {
   if (in_dim < 1 || in_dim > SWARM_POLICY_MAX_IN || out_dim < 2 || out_dim > SWARM_POLICY_MAX_OUT || (out_dim & 1))
     return pfail(SWARM_ELIMIT, "policy dims out of range"), (long long)SWARM_ELIMIT;
   if (precision == SWARM_POLICY_BF16) return (long long)Bf16Layout(out_dim).total;
+  if (precision == SWARM_POLICY_F32X3) return 2 * (long long)Bf16Layout(out_dim).total;  // hi blob, lo blob
   if (precision == SWARM_POLICY_F32) return (long long)F32Layout(in_dim).total * 4;
   return pfail(SWARM_EINVAL, "unknown precision"), (long long)SWARM_EINVAL;
 }
@@ -460,7 +727,41 @@ int swarm_policy_pack(int in_dim, int out_dim, int precision, const float* w1, c
   if (nb < 0) return (int)nb;
   if (!w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !host_out) return pfail(SWARM_ENULL, "null weight pointer");
   memset(host_out, 0, (size_t)nb);
-  if (precision == SWARM_POLICY_BF16) {
+  if (precision == SWARM_POLICY_F32X3) {
+    // the bf16 blob's fragment order twice, f16 elements: hi = f16(v), then lo = f16((v - hi) 2^11)
+    const Bf16Layout L(out_dim);
+    for (int part = 0; part < 2; ++part) {
+      unsigned char* base = static_cast<unsigned char*>(host_out) + part * L.total;
+      auto cv = [part](float v) -> uint16_t {
+        const uint16_t hi = f16_rne(v);
+        return part == 0 ? hi : f16_rne((v - f16_to_f32(hi)) * 2048.f);  // lo scaled by 2^11 (kernel: X3_LO_SCALE)
+      };
+      uint16_t* w1f = reinterpret_cast<uint16_t*>(base + L.w1);
+      uint16_t* w2f = reinterpret_cast<uint16_t*>(base + L.w2);
+      uint16_t* w3f = reinterpret_cast<uint16_t*>(base + L.w3);
+      for (int ob = 0; ob < OB; ++ob)
+        for (int l = 0; l < 64; ++l) {
+          const int m = ob * 32 + (l & 31), h = l >> 5;
+          for (int ks = 0; ks < KS1; ++ks)
+            for (int j = 0; j < 8; ++j) {
+              const int k = 16 * ks + 8 * h + j;
+              const float v = k < in_dim ? w1[m * in_dim + k] : (k == in_dim ? b1[m] : 0.f);
+              w1f[((ob * KS1 + ks) * 64 + l) * 8 + j] = cv(v);
+            }
+          for (int ks = 0; ks < KS2; ++ks)
+            for (int j = 0; j < 8; ++j) w2f[((ob * KS2 + ks) * 64 + l) * 8 + j] = cv(w2[m * H + chained_k(ks, h, j)]);
+        }
+      for (int ks = 0; ks < KS2; ++ks)
+        for (int h = 0; h < 2; ++h)
+          for (int m = 0; m < out_dim; ++m)
+            for (int j = 0; j < 8; ++j)
+              w3f[((ks * 2 * out_dim) + h * out_dim + m) * 8 + j] = cv(w3[m * H + chained_k(ks, h, j)]);
+      if (part == 0) {
+        memcpy(base + L.b2, b2, H * 4);
+        memcpy(base + L.b3, b3, (size_t)out_dim * 4);
+      }
+    }
+  } else if (precision == SWARM_POLICY_BF16) {
     const Bf16Layout L(out_dim);
     unsigned char* base = static_cast<unsigned char*>(host_out);
     uint16_t* w1f = reinterpret_cast<uint16_t*>(base + L.w1);
@@ -548,6 +849,16 @@ int swarm_policy_forward(const swarm_policy_t* p, const float* obs, long long ro
       return pfail(SWARM_EHIP, "hipFuncSetAttribute failed");
     const int grid = grid_for(BF16_WAVES_T, ((rows + 31) / 32 + BF16_TILES - 1) / BF16_TILES);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * BF16_WAVES_T), lds, s, a);
+  } else if (p->precision == SWARM_POLICY_F32X3) {
+    const int lds = (int)Bf16Layout(p->out_dim).total;
+    const bool dflt = p->in_dim == 37 && p->out_dim == 6;
+    (void)dflt;  // the compile-time-dims instance spills (71 VGPRs at 512); the runtime-dims one fits (492)
+    auto fn = policy_mlp_x3<X3_WAVES>;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+        hipSuccess)
+      return pfail(SWARM_EHIP, "hipFuncSetAttribute failed");
+    const int grid = grid_for(X3_WAVES, (rows + 31) / 32);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * X3_WAVES), lds, s, a);
   } else {
     const int grid = grid_for(F32_WAVES, (rows + 15) / 16) * 2;
     hipLaunchKernelGGL(policy_mlp_f32<F32_WAVES>, dim3(grid), dim3(64 * F32_WAVES), 0, s, a);

@@ -50,6 +50,7 @@ POLICY_MAX_IN = 47
 POLICY_MAX_OUT = 12
 POLICY_BF16 = 0
 POLICY_F32 = 1
+POLICY_F32X3 = 2
 POLICY_ACT_MEAN = 0
 POLICY_ACT_SAMPLE = 1
 EVAL_LIVE = 1

@@ -39,11 +39,21 @@ class GlobalStateGather:
     through pinned host memory on the side stream (synchronously, so no overlap there).
     A CPU ring (tests) is gathered in place.
 
+    Side stream (`stream`): "auto" (default) issues the gathers from the device's default stream
+    when no step launches on it (the env-group case), else from a new stream.  A rank then keeps
+    to the default stream, the G group streams and RCCL's own stream — 4 with 2 groups, within
+    the box's GPU_MAX_HW_QUEUES = 4 (a fifth active stream shares a hardware queue and
+    serialises behind it).  Anything else the caller queues on the side stream orders after the
+    gathers issued before it.  "new" forces a fresh stream; a torch.cuda.Stream is used as given.
+
     Usage per step k:  g.before_step(streams); <launch step k on streams>; g.after_step(streams, k in sched)
     then g.wait() before reading `g.result(i)` of the i-th gather on the current stream.
+    Buffer reuse: gather i + keep overwrites gather i's buffer.  It is ordered after every read
+    queued, before it is issued (host order), on a stream that called wait() or result():
+    each such stream records an event at that point and the side stream waits for it.
     """
 
-    def __init__(self, ring: torch.Tensor, select_slot, *, group=None, keep: int = 2):
+    def __init__(self, ring: torch.Tensor, select_slot, *, group=None, keep: int = 2, stream="auto"):
         if ring.dim() != 3:
             raise ValueError("ring must be [slots, E_local, F]")
         self.ring, self.select_slot, self.group = ring, select_slot, group
@@ -61,7 +71,13 @@ class GlobalStateGather:
         self.count = 0    # gathers issued
         self.gathered_steps: list[int] = []
         if self.cuda:
-            self.stream = torch.cuda.Stream(ring.device)
+            if not (stream in ("auto", "new") or isinstance(stream, torch.cuda.Stream)):
+                raise ValueError(f"stream must be 'auto', 'new' or a torch.cuda.Stream, not {stream!r}")
+            self._stream_mode = stream
+            # the side stream: chosen at the first gather ("auto" needs the launch streams)
+            self.stream = stream if isinstance(stream, torch.cuda.Stream) else None
+            self._consumers: list = []  # streams that results were handed to (wait / result)
+            self._consumer_evs: list = []
             self.slot_done = [torch.cuda.Event() for _ in range(self.slots)]
             self.slot_pending = [False] * self.slots
             self._step_evs: list = []
@@ -94,6 +110,14 @@ class GlobalStateGather:
         if not self.cuda:
             self._gather(out, src)
             return
+        if self.stream is None:
+            self.stream = self._pick_stream(streams)
+        if self.count > len(self.outs):
+            # `out` held gather count - 1 - keep: reads of it queued so far on the consumer
+            # streams finish before the gather rewrites it
+            for st, ev in zip(self._consumers, self._consumer_evs):
+                ev.record(st)
+                self.stream.wait_event(ev)
         while len(self._step_evs) < len(streams):
             self._step_evs.append(torch.cuda.Event())
         for st, ev in zip(streams, self._step_evs):
@@ -116,18 +140,40 @@ class GlobalStateGather:
         else:
             out.copy_(src, non_blocking=True)
 
+    def _pick_stream(self, streams) -> "torch.cuda.Stream":
+        if self._stream_mode == "auto" and not self.staged:
+            dflt = torch.cuda.default_stream(self.ring.device)
+            if all(st != dflt for st in streams):
+                return dflt
+        return torch.cuda.Stream(self.ring.device)
+
+    def _consumer(self) -> None:
+        """Register the current stream as a reader of the results (see the class doc)."""
+        if not self.cuda:
+            return
+        cur = torch.cuda.current_stream(self.ring.device)
+        if self.stream is not None and cur == self.stream:
+            return  # reads on the side stream are ordered before its next gather anyway
+        if all(cur != st for st in self._consumers):
+            self._consumers.append(cur)
+            self._consumer_evs.append(torch.cuda.Event())
+
     def wait(self) -> None:
         """Make the current stream wait for every gather issued so far."""
         if self.cuda:
-            torch.cuda.current_stream(self.ring.device).wait_stream(self.stream)
+            self._consumer()
+            if self.stream is not None:
+                torch.cuda.current_stream(self.ring.device).wait_stream(self.stream)
 
     def result(self, i: int = -1) -> torch.Tensor:
-        """Buffer of gather i (default: the latest); valid until `keep` further gathers."""
+        """Buffer of gather i (default: the latest).  Reads of it queued on the current stream
+        before gather i + keep is issued are ordered before that gather overwrites it."""
         if self.count == 0:
             raise RuntimeError("no gather issued yet")
         i = self.count - 1 if i < 0 else i
         if not self.count - len(self.outs) <= i < self.count:
             raise IndexError(f"gather {i} was overwritten (keep={len(self.outs)})")
+        self._consumer()
         return self.outs[i % len(self.outs)]
 
 

@@ -12,7 +12,9 @@ launches (policy, env step) with no host round trip:
     vec.step(acts)
 
 precision "bf16" (default): bf16 MFMA operands with f32 accumulation (~1e-2 relative on the
-logits); "f32": f32 MFMA (within summation-order rounding of the f32 graph).
+logits); "f32": f32 MFMA (within summation-order rounding of the f32 graph); "f32x3": the f32
+graph's accuracy on f16 MFMA — every operand split into f16 hi + lo, three products per term
+(hi*hi + hi*lo + lo*hi, ~2^-21 relative each); obs / weights / activations within the f16 range.
 """
 from __future__ import annotations
 
@@ -24,7 +26,7 @@ import torch
 from . import _native as nat
 from .onnx_weights import mlp_layers, read_onnx
 
-_PRECISION = {"bf16": nat.POLICY_BF16, "f32": nat.POLICY_F32}
+_PRECISION = {"bf16": nat.POLICY_BF16, "f32": nat.POLICY_F32, "f32x3": nat.POLICY_F32X3}
 
 
 def _fp(a: np.ndarray):
@@ -34,7 +36,7 @@ def _fp(a: np.ndarray):
 class PolicyMLP:
     def __init__(self, layers, *, device="cuda", precision: str = "bf16"):
         if precision not in _PRECISION:
-            raise ValueError(f"precision must be 'bf16' or 'f32', got {precision!r}")
+            raise ValueError(f"precision must be one of {sorted(_PRECISION)}, got {precision!r}")
         if len(layers) != 3:
             raise ValueError("expected 3 dense layers (two 256-unit relu hidden layers + logits)")
         (w1, b1, r1), (w2, b2, r2), (w3, b3, r3) = layers

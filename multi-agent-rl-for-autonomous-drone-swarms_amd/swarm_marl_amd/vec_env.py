@@ -589,7 +589,13 @@ class VecSwarm:
         With env groups: the kernel of group 0."""
         li = self.group_launch_info[0]
         kid = int(li.kernel_id)
-        if self.env_cfg is not None:  # per-env parameters: always the generic kernel
+        if self.env_cfg is not None:
+            # per-env parameters: launch() always takes the generic kernel, whose geometry the
+            # AUTO query does not describe (it reports the specialisation's) — query it as such
+            gp = nat.SwarmParams.from_buffer_copy(self._gparams[0])
+            gp.kernel_path = nat.PATH_GENERIC
+            li = nat.SwarmLaunchInfo()
+            nat.check(self.lib.swarm_query_launch(ctypes.byref(gp), ctypes.byref(li)), self.lib)
             kid = nat.KERNEL_GENERIC
         if kid == nat.KERNEL_STEP64_PERSISTENT and self.persistent:
             return "swarm_step64<32>"

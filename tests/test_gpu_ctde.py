@@ -86,6 +86,44 @@ def test_overlapped_gather_equals_synchronous(pg, e, n, groups, slots, every):
     assert torch.equal(a.obs, b.obs) and torch.equal(a.pos, b.pos)
 
 
+@pytest.mark.parametrize("mode", ["auto", "new"])
+def test_result_buffers_reused_after_consumer_reads(pg, mode):
+    """keep=1 < gathers: every gather overwrites the previous one's buffer.  The consumer queues
+    a copy of each result on the current stream right after wait() (no host sync); the gather
+    that reuses the buffer must order after that copy (consumer-stream event)."""
+    from swarm_marl_amd import VecSwarm
+    from swarm_marl_amd.distributed import GlobalStateGather, gather_global_state
+    dev = pg
+    e, n, steps = 256, 64, 9
+    kw = dict(device=dev, auto_reset=True, seed=5, with_global_state=True)
+    a = VecSwarm(e, {"num_drones": n}, groups=2, global_state_slots=2, **kw)
+    b = VecSwarm(e, {"num_drones": n}, **kw)
+    a.reset()
+    b.reset()
+    g = GlobalStateGather(a.global_state_ring, a.select_global_state_slot, keep=1, stream=mode)
+    acts = [_acts(dev, e, n, 50 + k) for k in range(steps)]
+    for st in a.group_streams:
+        st.wait_stream(torch.cuda.current_stream(dev))
+    got, ref = [], []
+    for k in range(steps):
+        g.before_step(a.group_streams)
+        for gi, st in enumerate(a.group_streams):
+            with torch.cuda.stream(st):
+                a.step_group(gi, acts[k])
+        g.after_step(a.group_streams, gather=True)
+        g.wait()
+        got.append(g.result().clone())  # queued on the current stream, read before the reuse
+        b.step(acts[k])
+        ref.append(gather_global_state(b.global_state).clone())
+    if mode == "auto":  # two env groups: the gathers go out from the default stream
+        assert g.stream == torch.cuda.default_stream(dev)
+    else:
+        assert g.stream != torch.cuda.default_stream(dev)
+    torch.cuda.synchronize()
+    for k in range(steps):
+        assert torch.equal(got[k], ref[k]), f"gather {k}"
+
+
 def test_bench_ctde_rehearsal_line_one_rank(pg, capsys):
     """bench.main's CTDE branch end to end on one rank (RCCL group of one): the gather runs every
     --gather-every steps inside the timed region and the line says so."""

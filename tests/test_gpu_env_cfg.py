@@ -55,6 +55,8 @@ def test_uniform_records_equal_no_records(dev, n, e, dyn, groups):
     b_vec = VecSwarm(e, cfg, device=dev, auto_reset=True, seed=11, dynamics=dyn, groups=groups)
     b_vec.set_env_config()  # records holding the batch config
     assert b_vec.kernel_name().startswith("swarm_kernel<")
+    if kp == "generic":  # the records path's name is the generic kernel's, lane mode included
+        assert b_vec.kernel_name() == a_vec.kernel_name()
     a_vec.reset()
     b_vec.reset()
     resets = 0

@@ -5,6 +5,8 @@ Oracle: the reference's exported actor graph (artifacts/policy.onnx, scripts/exp
 (tests/golden/policy_onnx.npz: random obs and real N=64 env obs).
 Tolerances (stated per path):
   f32  (v_mfma_f32_16x16x4_f32): |logit error| <= 1e-4 + 1e-5 |logit|  (summation order only)
+  f32x3 (three v_mfma_f32_32x32x16_f16 passes over f16 hi / lo splits): the same bound; its host
+       emulation from the packed blob sits at 0.1 of it (tests/test_policy_cpu.py)
   bf16 (v_mfma_f32_32x32x16_bf16): within 0.02 of the NumPy emulation of the same bf16 arithmetic
        (tests/test_policy_cpu.py) and within 0.3 of the f32 graph (logits span about -37 .. 66).
 """
@@ -38,9 +40,10 @@ def _pol(fx, dev, precision):
     return PolicyMLP(layers, device=dev, precision=precision)
 
 
-def test_f32_logits_vs_graph(dev, fx):
+@pytest.mark.parametrize("precision", ["f32", "f32x3"])
+def test_f32_logits_vs_graph(dev, fx, precision):
     layers, d = fx
-    pol = _pol(fx, dev, "f32")
+    pol = _pol(fx, dev, precision)
     got = pol.logits(torch.as_tensor(d["obs"]).to(dev)).cpu().numpy()
     ref = d["logits"]
     assert np.all(np.abs(got - ref) <= 1e-4 + 1e-5 * np.abs(ref)), np.abs(got - ref).max()
@@ -61,7 +64,7 @@ def test_bf16_logits_vs_emulation_and_graph(dev, fx):
     assert err.max() <= 0.3 and err.mean() <= 0.03, (err.max(), err.mean())
 
 
-@pytest.mark.parametrize("precision", ["bf16", "f32"])
+@pytest.mark.parametrize("precision", ["bf16", "f32", "f32x3"])
 def test_actions_are_gaussian_mean_and_ragged_rows(dev, fx, precision):
     layers, d = fx
     pol = _pol(fx, dev, precision)
@@ -82,9 +85,10 @@ def test_headline_batch_f32_vs_float64(dev, fx):
     vec.reset()
     g = torch.Generator(device=dev).manual_seed(3)
     vec.step(torch.rand((8192, 64, 3), device=dev, generator=g) * 2 - 1)
-    pol32, pol16 = _pol(fx, dev, "f32"), _pol(fx, dev, "bf16")
+    pol32, pol16, polx3 = _pol(fx, dev, "f32"), _pol(fx, dev, "bf16"), _pol(fx, dev, "f32x3")
     lg32 = pol32.logits(vec.obs).reshape(-1, 6)
     lg16 = pol16.logits(vec.obs).reshape(-1, 6)
+    lgx3 = polx3.logits(vec.obs).reshape(-1, 6)
     idx = torch.randperm(lg32.shape[0], device=dev, generator=g)[:4096]
     x = vec.obs.reshape(-1, 37)[idx].double().cpu().numpy()
     for i, (w, b, relu) in enumerate(layers):
@@ -93,6 +97,8 @@ def test_headline_batch_f32_vs_float64(dev, fx):
             x = np.maximum(x, 0)
     got32 = lg32[idx].double().cpu().numpy()
     assert np.all(np.abs(got32 - x) <= 1e-4 + 1e-5 * np.abs(x)), np.abs(got32 - x).max()
+    gotx3 = lgx3[idx].double().cpu().numpy()  # the three-pass f16 path meets the f32 tolerance
+    assert np.all(np.abs(gotx3 - x) <= 1e-4 + 1e-5 * np.abs(x)), np.abs(gotx3 - x).max()
     assert np.abs(lg16[idx].double().cpu().numpy() - x).max() <= 0.3
 
 

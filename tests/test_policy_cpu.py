@@ -280,3 +280,87 @@ def test_pack_rejects_bad_dims():
     assert lib.swarm_policy_packed_bytes(37, 14, 0) < 0
     assert lib.swarm_policy_packed_bytes(37, 5, 0) < 0
     assert lib.swarm_policy_packed_bytes(37, 6, 7) < 0
+
+
+def _split16(x: np.ndarray):
+    """f32 -> (hi, lo) f16 pieces as the f32x3 kernel splits its activations (RNE both; lo is
+    (x - hi) scaled by 2^11)."""
+    x = np.asarray(x, np.float32)
+    hi = x.astype(np.float16)
+    lo = ((x - hi.astype(np.float32)) * np.float32(2048)).astype(np.float16)
+    return hi.astype(np.float64), lo.astype(np.float64)
+
+
+def emulate_x3_kernel(buf: np.ndarray, x: np.ndarray, out: int) -> np.ndarray:
+    """The f32x3 kernel's arithmetic in float64 from its packed blob (hi blob then lo blob, the
+    bf16 blob's fragment maps with f16 elements): every layer sums hi*hi + hi*lo + lo*hi."""
+    total = len(buf) // 2
+    rows, d = x.shape
+
+    def frags(part):
+        b = buf[part * total:(part + 1) * total]
+        w1 = b[:8 * 3 * 1024].view(np.float16).astype(np.float64).reshape(8, 3, 2, 32, 8)
+        off = 8 * 3 * 1024
+        w2 = b[off:off + 8 * 16 * 1024].view(np.float16).astype(np.float64).reshape(8, 16, 2, 32, 8)
+        off += 8 * 16 * 1024
+        w3 = b[off:off + 16 * 2 * out * 16].view(np.float16).astype(np.float64).reshape(16, 2, out, 8)
+        off += 16 * 2 * out * 16
+        return w1, w2, w3, b[off:off + 1024].view(np.float32), b[off + 1024:off + 1024 + 4 * out].view(np.float32)
+
+    (w1h, w2h, w3h, b2, b3), (w1l, w2l, w3l, _, _) = frags(0), frags(1)
+    xp = np.zeros((rows, 48), np.float32)
+    xp[:, :d] = x
+    xp[:, d] = 1.0
+    xh, xl = _split16(xp)
+    xh, xl = xh.reshape(rows, 3, 2, 8), xl.reshape(rows, 3, 2, 8)
+    reg_row = np.array([[(i & 3) + 8 * (i >> 2) + 4 * h for i in range(16)] for h in range(2)])
+
+    def chain(c):
+        obn = c.shape[0]
+        frag = np.zeros((2 * obn, 2, c.shape[2], 8), np.float32)
+        for ob in range(obn):
+            for s in range(2):
+                for h in range(2):
+                    for j in range(8):
+                        frag[2 * ob + s, h, :, j] = c[ob, reg_row[h, 8 * s + j], :]
+        return _split16(np.maximum(frag, 0))
+
+    def x3(eq, ah, al, bh, bl):  # hi*hi + 2^-11 (hi*lo + lo*hi)
+        return np.einsum(eq, ah, bh) + (np.einsum(eq, ah, bl) + np.einsum(eq, al, bh)) / 2048.0
+
+    c1 = x3("oshmj,nshj->omn", w1h, w1l, xh, xl).astype(np.float32)
+    h1h, h1l = chain(c1)
+    c2 = (x3("okhmj,khnj->omn", w2h, w2l, h1h, h1l) + b2.reshape(8, 32, 1)).astype(np.float32)
+    h2h, h2l = chain(c2)
+    c3 = x3("khmj,khnj->mn", w3h, w3l, h2h, h2l) + b3[:, None]
+    return c3.T
+
+
+def test_pack_f32x3_split_and_emulation_meet_the_f32_tolerance():
+    """The f32x3 blob: hi = f16(w) (RNE, as numpy), lo = f16(w - hi); its three-pass arithmetic
+    (emulated in float64 from the blob) is within the f32 path's tolerance of the f32 graph."""
+    from swarm_marl_amd import _native as nat
+    lib = nat.load_library()
+    layers, d = fixture_layers()
+    buf = _pack(lib, layers, nat.POLICY_F32X3)
+    assert len(buf) == 2 * lib.swarm_policy_packed_bytes(37, 6, nat.POLICY_BF16)
+    (w1, b1, _), (w2, b2, _), _ = layers
+    half = len(buf) // 2
+    hi2 = buf[8 * 3 * 1024:8 * 19 * 1024].view(np.float16).reshape(8, 16, 2, 32, 8)
+    lo2 = buf[half + 8 * 3 * 1024:half + 8 * 19 * 1024].view(np.float16).reshape(8, 16, 2, 32, 8)
+    # out block 3, k-step 5, half 1, row 7, element 2 -> W2[3*32+7][chained_k(5, 1, 2)]
+    ks, h, j = 5, 1, 2
+    k = (ks >> 1) * 32 + 16 * (ks & 1) + 8 * (j >> 2) + 4 * h + (j & 3)
+    w = np.float32(w2[3 * 32 + 7, k])
+    assert hi2[3, ks, h, 7, j] == np.float16(w)
+    assert lo2[3, ks, h, 7, j] == np.float16((w - np.float32(np.float16(w))) * np.float32(2048))
+    rec = hi2.astype(np.float64) + lo2.astype(np.float64) / 2048.0
+    w2perm = np.array([[w2[ob * 32 + m, (s >> 1) * 32 + 16 * (s & 1) + 8 * (jj >> 2) + 4 * hh + (jj & 3)]
+                        for ob in range(8) for s in range(16) for hh in range(2) for m in range(32)
+                        for jj in range(8)]], np.float64).reshape(rec.shape)
+    big = np.abs(w2perm) > 1e-4
+    assert np.all(np.abs(rec - w2perm)[big] <= 2.0 ** -21 * np.abs(w2perm)[big])
+    obs = d["obs"][::3]
+    got = emulate_x3_kernel(buf, obs, 6)
+    ref = d["logits"][::3]
+    assert np.all(np.abs(got - ref) <= 1e-4 + 1e-5 * np.abs(ref)), np.abs(got - ref).max()

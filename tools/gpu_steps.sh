@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 GPU step runner: bash tools/gpu_r03.sh <tag> <name>:<timeout>:<command> ...
+# GPU step runner: bash tools/gpu_steps.sh <tag> <name>:<timeout>:<command> ...
 # Every step runs under its own timeout; the first failing step ends the call (no retries).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
