@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SWARM_ABI_VERSION 4
+#define SWARM_ABI_VERSION 5
 
 /* error codes */
 #define SWARM_OK 0
@@ -194,6 +194,13 @@ typedef struct swarm_out {
   float* dist_goal;      /* [E,N]   optional: infos["distance_to_goal"] */
   uint8_t* info_flags;   /* [E,N]   optional: SWARM_AGENT_* bits */
   float* global_state;   /* [E,6N+3] optional: concat(pos, vel, goal) (drone_swarm_env.py:293-302) */
+  const struct swarm_eval* eval;  /* optional HOST pointer to an eval tracker's state (swarm_eval_t,
+                             its `flags` holding SWARM_EVAL_STEP_FUSED): the step accumulates the
+                             evaluation protocol's per-step terms in its write-back — episode reward,
+                             steps, first all-reached step, collision vote, path length — and
+                             swarm_eval_update then adds only the formation error and closes the
+                             ended episodes.  Kinematic swarm_step64 launches only (SWARM_KERNEL_STEP64
+                             from swarm_query_launch, no env_cfg): other launches return SWARM_EINVAL */
 } swarm_out_t;
 
 /* Launch geometry actually used (for tests / profiling). */
@@ -320,6 +327,7 @@ const char* swarm_policy_last_error(void);
  */
 #define SWARM_EVAL_LIVE 1u       /* status: an episode is being accumulated */
 #define SWARM_EVAL_COLLIDED 2u   /* status: an observed agent reported a collision */
+#define SWARM_EVAL_STEP_FUSED 1  /* swarm_eval_t.flags: per-step accumulation done by the step (out.eval) */
 #define SWARM_EVAL_RECORD 9      /* doubles per record: global env index, success, collision_free, time_to_goal
                                     (NaN if never all-reached), formation_error, path_efficiency,
                                     episode_reward, steps, update_index of the closing update */
@@ -343,6 +351,7 @@ typedef struct swarm_eval {
                              rest are dropped) */
   int32_t capacity;       /* a multiple of SWARM_EVAL_SEGMENTS */
   int32_t update_index;   /* stamped into the records this update closes (the caller counts updates) */
+  int32_t flags;          /* SWARM_EVAL_STEP_FUSED: the step launches carry this state in out.eval */
   const float* state_pos;   /* [E,N,3] optional: the env state's positions after the step (bitwise
                                obs[..., 0:3]), read contiguously instead of from the obs rows */
   const float* state_goal;  /* [E,3] optional (with state_pos): the goal; obs[..., 6:9] = goal - pos */

@@ -154,6 +154,10 @@ __global__ void __launch_bounds__(EVAL_THREADS * EVAL_WG_ENVS) eval_update_kerne
   const bool ends = (done & (SWARM_ENV_TERMINATED | SWARM_ENV_TRUNCATED)) != 0 && SWARM_EVAL_ABLATE != 2 &&
                     SWARM_EVAL_ABLATE != 4;
   const bool restarts = ends && (done & SWARM_ENV_RESET) != 0;
+  // SWARM_EVAL_STEP_FUSED: the step launch (out.eval) already added this step's reward, steps,
+  // reached step, collision vote and path lengths (swarm_kernel.hip s64_env, the same arithmetic):
+  // only the formation error and the episode ends are left here
+  const bool fused = (v.flags & SWARM_EVAL_STEP_FUSED) != 0;
   // ---- per-agent votes, path length, observed positions; path efficiency and the next
   // episode's start rows when the episode ends here
   double rsum = 0.0, pe = 0.0;
@@ -161,9 +165,28 @@ __global__ void __launch_bounds__(EVAL_THREADS * EVAL_WG_ENVS) eval_update_kerne
   for (int i = t; i < a.N; i += EVAL_THREADS) {
     const size_t r = (size_t)e * a.N + i;
     const uint8_t fl = a.info_flags[r];
-    const float rw = a.reward[r];
     float ox, oy, oz;
     obs_pos(a, r, ox, oy, oz);
+    if (fused) {  // observed positions for the formation error; the ended episode's path efficiency
+      const bool has = (fl & SWARM_AGENT_HAS_OBS) != 0;
+      n_obs += has ? 1 : 0;
+      pos[i] = has ? make_float4(ox, oy, oz, 1.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ends) {
+        const double tr = v.traveled[r];
+        const float straight = norm1d(v.start[3 * r] - v.goal[3 * r], v.start[3 * r + 1] - v.goal[3 * r + 1],
+                                      v.start[3 * r + 2] - v.goal[3 * r + 2]);
+        pe += tr > 1e-8 ? (double)straight / tr : 0.0;
+      }
+      if (restarts) {
+        float rx, ry, rz;
+        obs_goal_vec(a, e, r, ox, oy, oz, rx, ry, rz);
+        v.start[3 * r] = ox; v.start[3 * r + 1] = oy; v.start[3 * r + 2] = oz;
+        v.goal[3 * r] = ox + rx; v.goal[3 * r + 1] = oy + ry; v.goal[3 * r + 2] = oz + rz;
+        v.traveled[r] = 0.0;
+      }
+      continue;
+    }
+    const float rw = a.reward[r];
     const float lx = v.last[3 * r], ly = v.last[3 * r + 1], lz = v.last[3 * r + 2];
     double tr = v.traveled[r];
     float sx = 0.f, sy = 0.f, sz = 0.f, gx = 0.f, gy = 0.f, gz = 0.f, rx = 0.f, ry = 0.f, rz = 0.f;
@@ -250,14 +273,15 @@ __global__ void __launch_bounds__(EVAL_THREADS * EVAL_WG_ENVS) eval_update_kerne
   }
   if (ends) pe = wave_sum(pe) / (double)a.N;
   if (t != 0) return;
-  const double ep_reward = ep_reward0 + (n_st > 0 ? rsum / (double)n_st : 0.0);
+  const double ep_reward = fused ? ep_reward0 : ep_reward0 + (n_st > 0 ? rsum / (double)n_st : 0.0);
   const double fe_sum = fe_sum0 + fe;
-  const int steps = steps0 + 1;
+  const int steps = fused ? steps0 : steps0 + 1;
   int reached = reached0;
-  if (!not_reached && reached < 0) reached = steps;
+  if (!fused && !not_reached && reached < 0) reached = steps;
   if (!ends) {
-    v.ep_reward[e] = ep_reward;
     v.fe_sum[e] = fe_sum;
+    if (fused) return;
+    v.ep_reward[e] = ep_reward;
     v.ep_steps[e] = steps;
     v.reached_step[e] = reached;
     if (coll) v.status[e] = status | SWARM_EVAL_COLLIDED;
@@ -360,6 +384,7 @@ int make_args(const swarm_params_t* p, const swarm_eval_t* ev, const swarm_out_t
     return efail(SWARM_ENULL, "an eval state buffer is NULL");
   if ((ev->state_pos == nullptr) != (ev->state_goal == nullptr))
     return efail(SWARM_EINVAL, "state_pos and state_goal go together");
+  if (ev->flags & ~SWARM_EVAL_STEP_FUSED) return efail(SWARM_EINVAL, "unknown eval flags 0x%x", (unsigned)ev->flags);
   if (ev->capacity < 0 || ev->capacity % SWARM_EVAL_SEGMENTS != 0)
     return efail(SWARM_EINVAL, "capacity must be a non-negative multiple of %d", SWARM_EVAL_SEGMENTS);
   a->E = p->num_envs;

@@ -1714,12 +1714,22 @@ struct S64In {
 // phase by phase (s64_args: an opaque copy of the kernarg pointer, so the compiler cannot keep
 // the ~40 loop-invariant parameters and pointers live in SGPRs across the persistent loop and
 // spill them; scalar-cache hits cost a few cycles).
+// The eval tracker's per-step accumulators (swarm_out_t.eval, SWARM_EVAL_STEP_FUSED): device
+// pointers of this launch's env rows, NULL status = off.
+struct S64Eval {
+  double* ep_reward;
+  int32_t* ep_steps;
+  int32_t* reached_step;
+  uint8_t* status;
+  double* traveled;
+};
 struct S64Args {
   KParams P;
   swarm_state_t S;
   const float* actions;
   const uint8_t* amask;
   swarm_out_t O;
+  S64Eval EV;
 };
 #define KARG __attribute__((address_space(4)))
 typedef const KARG S64Args* S64ArgPtr;
@@ -2069,6 +2079,37 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     A->O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
                                 (do_reset ? SWARM_ENV_RESET : 0u));
   const uint64_t m_term = __ballot(term), m_trunc = __ballot(trunc);
+  if (DYN == DYN_KIN && A->EV.status != nullptr) {
+    // fused eval: swarm_eval_update's per-step part (swarm_eval.hip eval_update_kernel, the same
+    // arithmetic and f64 butterfly): episode reward += mean reward of the stepped agents, steps,
+    // the first step all observed agents reached, the collision vote, path lengths
+    const uint8_t status = A->EV.status[env];
+    if (status & SWARM_EVAL_LIVE) {
+      double rsum = (double)rew;  // 0 for agents without a reward entry
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) rsum += __shfl_xor(rsum, o);
+      const bool coll = __ballot(cont && collided) != 0;
+      const bool not_reached = __ballot(cont && !reached) != 0;
+      if (cont) {
+        // path length += |last - p| (evaluate_protocol.py's _distance: the sdot-double norm); last =
+        // the position this step started from, still in the state (written back below): an agent
+        // observed now was observed at the previous step or stands at its episode's start
+        const float* po = A->S.pos + ea * 3 + t3;
+        const float inc = sqrt_rn(sqsum_1d(po[0] - px, po[1] - py, po[2] - pz));
+        double* tr = A->EV.traveled + ea + t;
+        *tr = *tr + (double)inc;
+      }
+      if (t == 0) {
+        const int steps = A->EV.ep_steps[env] + 1;
+        int rs = A->EV.reached_step[env];
+        if (!not_reached && rs < 0) rs = steps;
+        A->EV.ep_reward[env] = A->EV.ep_reward[env] + (n_active > 0 ? rsum / (double)n_active : 0.0);
+        A->EV.ep_steps[env] = steps;
+        A->EV.reached_step[env] = rs;
+        if (coll) A->EV.status[env] = (uint8_t)(status | SWARM_EVAL_COLLIDED);
+      }
+    }
+  }
   STAMP_AT(srec, 5);
   A = s64_args();
 
@@ -3312,6 +3353,20 @@ __device__ __forceinline__ uint32_t h_finish_fast(const uint32_t (&nk)[4], const
          (ok_ob ? 0u : S64F_BOUND_OB);
 }
 
+// Phase stamps of step256 (diagnostic stamps build, tools/stamps.py with SWARM_STAMPS_KERNEL=n256):
+// wave 0's view of each phase boundary, one record per env
+#ifdef SWARM_STAMPS
+#define STAMP256(i)                                                                      \
+  do {                                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+    unsigned long long ts_;                                                              \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");           \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+    if (threadIdx.x == 0 && env < (1 << 16)) g_stamps[env * 16 + (i)] = ts_;             \
+  } while (0)
+#else
+#define STAMP256(i) do {} while (0)
+#endif
 #if SWARM_HAS_PART(7)  // emitted in its own translation unit only
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) swarm_step256(const S64Args args) {
   (void)args;  // read through s64_args()
@@ -3324,6 +3379,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   if (env >= A->P.E) return;  // whole block
   const int M = A->P.M;
   const size_t ag = (size_t)env * H_N + i;
+  STAMP256(0);
+#ifdef SWARM_STAMPS
+  if (i == 0 && env < (1 << 16)) g_stamps[env * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+#endif
 
   // ---- loads
   const float gx0 = A->S.goal[3 * env], gy0 = A->S.goal[3 * env + 1], gz0 = A->S.goal[3 * env + 2];
@@ -3342,6 +3401,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   }
   float gx = gx0, gy = gy0, gz = gz0;
   const int n_active = __syncthreads_count(act);
+  STAMP256(1);
   A = s64_args();
 
   // ---- integrate: drone_swarm_env.py:98-117 (swarm_kernel, DYN_KIN)
@@ -3375,6 +3435,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   }
   h_put(L, w, t, px, py, pz, act ? 1.f : 0.f);
   const bool fast = __syncthreads_and(act) != 0;  // also the barrier after the puts
+  STAMP256(2);
   A = s64_args();
 
   // ---- formation + minimum pass (every pair once), obstacle pass
@@ -3387,12 +3448,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
   bool ocoll = false;
   obstacle_pass_s64<MSL, true>(L.osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
+  STAMP256(3);
   __syncthreads();  // handed-over sums / minima written
   fsum += (double)L.x.p1.sum[0][i];
   fsum += (double)L.x.p1.sum[1][i];
   smin = fminf(smin, fminf(L.x.p1.mn[0][i], L.x.p1.mn[1][i]));
   A = s64_args();
 
+  STAMP256(4);
   // ---- rewards / terminations: drone_swarm_env.py:120-172 (swarm_kernel, DYN_KIN)
   bool pcoll = smin <= A->P.thr_pair * FAST_LO;
   if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act)
@@ -3449,6 +3512,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     A->O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
                                    (do_reset ? SWARM_ENV_RESET : 0u));
 
+  STAMP256(5);
   // ---- in-kernel auto-reset (block-uniform): the new episode, then its keys
   uint32_t episode_new = episode0;
   if (do_reset) {
@@ -3483,6 +3547,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     bool c2 = false;
     obstacle_pass_s64<MSL, false>(L.osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
   }
+  STAMP256(6);
   A = s64_args();
   uint32_t nk[KS];
 #pragma unroll
@@ -3513,6 +3578,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
       if (slow_ob) exact_select<MSL, true>(L.obst, M, -1, H_MS, max_first(od, H_MS), px, py, pz, od, oj);
     }
   }
+  STAMP256(7);
   A = s64_args();
 
   // ---- state write-back
@@ -3555,6 +3621,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     const float4 q = L.obst[oj[s] & (H_MMAX - 1)];
     row[21 + 4 * s] = q.x - px; row[22 + 4 * s] = q.y - py; row[23 + 4 * s] = q.z - pz; row[24 + 4 * s] = od[s];
   }
+  STAMP256(8);
+#ifdef SWARM_STAMPS
+  if (i == 0 && env < (1 << 16)) {
+    g_stamps[env * 16 + 9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+    g_stamps[env * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    g_stamps[env * 16 + 12] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 #endif
 
@@ -3877,12 +3951,27 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   // ballot-packed byte outputs need N == 64 and dword-aligned bool tensors
   kp.pack_bytes = (kp.N == 64 && mode == MODE_STEP && ((uintptr_t)o->terminated | (uintptr_t)o->truncated |
                                                        (uintptr_t)s->active) % 4 == 0) ? 1 : 0;
+  S64Eval ev{nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (o->eval) {
+    // fused eval accumulation: the kinematic one-wave-per-env step64 launch only
+    const swarm_eval_t* e = o->eval;
+    const bool once = mode == MODE_STEP && step64_applies(p, kp) && kp.obs_vec4 && kp.pack_bytes && !s->env_cfg &&
+                      p->dynamics == DYN_KIN && !(s->work && step64_grid(p, kp.E) < kp.E);
+    if (!once)
+      return fail(SWARM_EINVAL, "out.eval (fused eval accumulation) needs the kinematic swarm_step64 launch "
+                                "(N = 64, K = 3, Ms = 4, no env_cfg, no persistent grid)");
+    if (!(e->flags & SWARM_EVAL_STEP_FUSED)) return fail(SWARM_EINVAL, "out.eval without SWARM_EVAL_STEP_FUSED in its flags");
+    if (!e->ep_reward || !e->ep_steps || !e->reached_step || !e->status || !e->traveled)
+      return fail(SWARM_ENULL, "out.eval: an accumulator buffer is NULL");
+    if (!o->info_flags) return fail(SWARM_ENULL, "out.eval needs out.info_flags (swarm_eval_update reads them)");
+    ev = S64Eval{e->ep_reward, e->ep_steps, e->reached_step, e->status, e->traveled};
+  }
   if (mode == MODE_STEP && step64_applies(p, kp) && kp.obs_vec4 && kp.pack_bytes && !s->env_cfg) {
     swarm_state_t st = *s;
     const bool phys = p->dynamics == DYN_PHYS;  // physics: the one-wave-per-env launch only
     const int grid = phys ? kp.E : step64_grid(p, kp.E);
     if (grid >= kp.E) st.work = nullptr;  // one env per workgroup: nothing to dequeue
-    const S64Args args{kp, st, actions, amask, *o};
+    const S64Args args{kp, st, actions, amask, *o, ev};
     if (st.work)
       hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step64(true, false)), dim3(grid), dim3(64), 0,
                          (hipStream_t)stream, args);
@@ -3896,7 +3985,7 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   }
   if (mode == MODE_STEP && step16q_applies(p, kp) && !s->env_cfg && ((uintptr_t)o->obs) % 16 == 0 &&
       ((uintptr_t)o->terminated | (uintptr_t)o->truncated | (uintptr_t)s->active) % 4 == 0) {
-    const S64Args args{kp, *s, actions, amask, *o};
+    const S64Args args{kp, *s, actions, amask, *o, ev};
     hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step16q()), dim3((kp.E + Q_WG_ENVS - 1) / Q_WG_ENVS),
                        dim3(64 * Q_WG_ENVS), 0, (hipStream_t)stream, args);
     hipError_t e = hipGetLastError();
@@ -4124,6 +4213,16 @@ int swarm_step_groups(const swarm_params_t* p, const swarm_state_t* s, const flo
     sg.env_cfg = row(s->env_cfg, 1);
     sg.env_cfg_next = row(s->env_cfg_next, 1);
     swarm_out_t og = *o;
+    swarm_eval_t eg;  // the eval accumulators of the group's rows (fused eval)
+    if (o->eval) {
+      eg = *o->eval;
+      eg.ep_reward = row(eg.ep_reward, 1);
+      eg.ep_steps = row(eg.ep_steps, 1);
+      eg.reached_step = row(eg.reached_step, 1);
+      eg.status = row(eg.status, 1);
+      eg.traveled = row(eg.traveled, N);
+      og.eval = &eg;
+    }
     og.obs = row(o->obs, N * D);
     og.reward = row(o->reward, N);
     og.terminated = row(o->terminated, N);

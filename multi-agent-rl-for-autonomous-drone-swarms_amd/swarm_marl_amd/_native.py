@@ -14,7 +14,7 @@ LIB_NAME = "libswarm_mi355x.so"
 LIB_DIR = Path(__file__).resolve().parent / "_lib"
 LIB_PATH = LIB_DIR / LIB_NAME
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 WORK_WORDS = 256  # SWARM_WORK_WORDS: u32 env-queue heads of the persistent swarm_step64
 
 PATH_AUTO = 0
@@ -55,6 +55,7 @@ POLICY_ACT_MEAN = 0
 POLICY_ACT_SAMPLE = 1
 EVAL_LIVE = 1
 EVAL_COLLIDED = 2
+EVAL_STEP_FUSED = 1
 EVAL_RECORD = 9
 EVAL_SEGMENTS = 64
 
@@ -137,7 +138,7 @@ class SwarmEnvOverrides(ctypes.Structure):
 class SwarmOut(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name in
                 ("obs", "reward", "terminated", "truncated", "env_done", "dist_goal",
-                 "info_flags", "global_state")]
+                 "info_flags", "global_state", "eval")]  # eval: host pointer to a SwarmEval (fused)
 
 
 class SwarmPolicy(ctypes.Structure):
@@ -149,6 +150,7 @@ class SwarmEval(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name in
                 ("ep_reward", "ep_steps", "reached_step", "status", "fe_sum", "start", "goal", "last",
                  "traveled", "records", "count")] + [("capacity", ctypes.c_int32), ("update_index", ctypes.c_int32),
+                                                     ("flags", ctypes.c_int32),
                                                      ("state_pos", ctypes.c_void_p), ("state_goal", ctypes.c_void_p)]
 
 

@@ -52,7 +52,14 @@ def aggregate_records(rec: np.ndarray) -> dict:
 
 
 class EvalTracker:
-    def __init__(self, vec: VecSwarm, capacity: int = 65536):
+    """fused (default "auto"): where the step runs the kinematic swarm_step64 kernel (N = 64,
+    K = 3, Ms = 4, no per-env records), the step itself accumulates the per-step terms in its
+    write-back (out.eval, SWARM_EVAL_STEP_FUSED: episode reward, steps, reached step, collision
+    vote, path length) and update() adds only the formation error and closes ended episodes —
+    same records (tests/test_gpu_eval.py).  Every step of the VecSwarm then accumulates, so
+    update() must follow every step (as without fusion); `detach()` ends the fusion."""
+
+    def __init__(self, vec: VecSwarm, capacity: int = 65536, fused="auto"):
         if vec.info_flags is None:
             raise ValueError("EvalTracker needs a VecSwarm built with with_infos=True")
         if vec.dynamics != "kinematic":
@@ -89,9 +96,44 @@ class EvalTracker:
         # positions / goal from the state tensors (contiguous) rather than the strided obs rows
         c.state_pos, c.state_goal = vec.pos.data_ptr(), vec.goal.data_ptr()
         self._c = c
+        if fused == "auto":
+            li = vec.group_launch_info[0]
+            fused = (vec.dynamics == "kinematic" and vec.env_cfg is None and int(li.kernel_id) == nat.KERNEL_STEP64)
+        self.fused = bool(fused)
+        self._step_c = []
+        if self.fused:
+            c.flags = nat.EVAL_STEP_FUSED
+            self._attach()
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.vec.device).cuda_stream
+
+    def _attach(self) -> None:
+        """Point every group's step launch at this tracker's accumulators (out.eval): group g's
+        struct holds its row offsets (swarm_step_groups offsets group 0's by itself)."""
+        vec = self.vec
+        self._step_c = [self._group_c(g) for g in range(vec.groups)]
+        for g, sc in enumerate(self._step_c):
+            sc.flags = nat.EVAL_STEP_FUSED
+            vec._gout[g].eval = ctypes.addressof(sc)
+        vec._eval_owner = self  # the structs and tensors stay alive while the VecSwarm writes them
+
+    def detach(self) -> None:
+        """Stop the fused accumulation (the steps no longer touch this tracker); update() then
+        accumulates every per-step term itself again."""
+        if not self.fused:
+            return
+        for g in range(self.vec.groups):
+            self.vec._gout[g].eval = None
+        if getattr(self.vec, "_eval_owner", None) is self:
+            self.vec._eval_owner = None
+        self.vec.join()
+        self.fused = False
+        self._c.flags = 0
+        self._step_c = []
+        # unfused updates measure path increments from `last`, which the fused steps did not keep:
+        # the state positions are where every agent observed next stands now
+        self.last.copy_(self.vec.pos)
 
     def begin(self, env_mask: torch.Tensor | None = None) -> None:
         """Open an episode in the masked envs (all if None) from the current observations."""
@@ -133,6 +175,7 @@ class EvalTracker:
             setattr(c, name, t.data_ptr() + lo * t.stride(0) * t.element_size())
         c.records, c.count, c.capacity = self.records_buf.data_ptr(), self.count.data_ptr(), self.capacity
         c.update_index = self.updates
+        c.flags = self._c.flags
         v = self.vec
         c.state_pos = v.pos.data_ptr() + lo * v.pos.stride(0) * v.pos.element_size()
         c.state_goal = v.goal.data_ptr() + lo * v.goal.stride(0) * v.goal.element_size()

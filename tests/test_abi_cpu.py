@@ -60,7 +60,7 @@ def _params(nat, lib, **kw):
 
 def test_abi_version_and_defaults(nat, lib):
     from swarm_marl_amd.envs.common import DroneEnvConfig
-    assert lib.swarm_abi_version() == nat.ABI_VERSION == 4
+    assert lib.swarm_abi_version() == nat.ABI_VERSION == 5
     p = _params(nat, lib)
     c = DroneEnvConfig()
     for name in ("max_steps", "num_obstacles", "sensed_obstacles", "neighbor_k"):
@@ -228,3 +228,23 @@ def test_step_groups_validation(nat, lib):
     p0 = _params(nat, lib, num_envs=0)
     zero = (ctypes.c_int32 * 2)(0, 0)
     assert lib.swarm_step_groups(ctypes.byref(p0), *args, 2, zero, streams) == 0
+
+
+@pytest.mark.parametrize("ctype,cname", [("SwarmOut", "swarm_out_t"), ("SwarmEval", "swarm_eval_t"),
+                                         ("SwarmParams", "swarm_params_t"), ("SwarmPolicy", "swarm_policy_t"),
+                                         ("SwarmLaunchInfo", "swarm_launch_info_t")])
+def test_struct_layouts_match_header(nat, tmp_path, ctype, cname):
+    """Every ctypes mirror of a header struct has the C compiler's size and field offsets."""
+    cls = getattr(nat, ctype)
+    fields = [f for f, _ in cls._fields_]
+    src = tmp_path / "layout.c"
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "swarm_mi355x.h"', "int main(void) {",
+             f'printf("%zu\\n", sizeof({cname}));']
+    lines += [f'printf("%zu\\n", offsetof({cname}, {f}));' for f in fields]
+    lines += ["return 0; }"]
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
+    out = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert out[0] == ctypes.sizeof(cls)
+    assert out[1:] == [getattr(cls, f).offset for f in fields]

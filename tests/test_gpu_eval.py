@@ -117,6 +117,54 @@ def test_eval_auto_reset_matches_oracle(dev):
         _cmp_summary(row, s, st, i)
 
 
+def _run_tracker(dev, fused, groups, native_groups=False, e=64, steps=70):
+    from swarm_marl_amd import VecSwarm
+    from swarm_marl_amd.eval_metrics import EvalTracker
+    vec = VecSwarm(e, {"num_drones": 64, "max_steps": 30}, device=dev, auto_reset=True, seed=17, with_infos=True,
+                   groups=groups)
+    vec.reset()
+    ev = EvalTracker(vec, capacity=8192, fused=fused)
+    assert ev.fused == fused
+    ev.begin()
+    g = torch.Generator(device=dev).manual_seed(23)
+    for _ in range(steps):
+        a = torch.rand((e, 64, 3), device=dev, generator=g) * 2 - 1
+        if native_groups:  # bench.py's launch: one swarm_step_groups call, group streams, no joins
+            vec.fork_groups()
+            vec.step_groups(a)
+            vec.join()
+        else:
+            vec.step(a)
+        ev.update()
+    assert vec.kernel_name() == "swarm_step64_once<32, 4>"
+    return ev.records()
+
+
+@pytest.mark.parametrize("groups,native", [(1, False), (2, False), (2, True)])
+def test_fused_eval_equals_unfused(dev, groups, native):
+    """SWARM_EVAL_STEP_FUSED (the step accumulates reward / steps / votes / path length in its
+    write-back, swarm_eval_update only the formation error): the same records, bit for bit, as
+    the unfused update at the headline shape (N = 64, swarm_step64_once), with env groups too."""
+    a = _run_tracker(dev, True, groups, native)
+    b = _run_tracker(dev, False, 1)
+    assert len(a) > 64 and a.shape == b.shape
+    assert np.array_equal(a, b, equal_nan=True)
+
+
+def test_fused_eval_needs_step64(dev):
+    """out.eval on a launch other than the kinematic step64 one is refused (SWARM_EINVAL)."""
+    from swarm_marl_amd import VecSwarm
+    from swarm_marl_amd.eval_metrics import EvalTracker
+    vec = VecSwarm(8, {"num_drones": 16}, device=dev, auto_reset=True, with_infos=True)
+    vec.reset()
+    assert EvalTracker(vec).fused is False  # auto: not the step64 kernel
+    ev = EvalTracker(vec, fused=True)
+    with pytest.raises(ValueError, match="step64"):
+        vec.step(torch.zeros((8, 16, 3), device=dev))
+    ev.detach()
+    vec.step(torch.zeros((8, 16, 3), device=dev))
+
+
 def test_curriculum_runner_stages(dev):
     from swarm_marl_amd.curriculum import CurriculumRunner
     from tests.test_eval_cpu import STAGES

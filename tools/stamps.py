@@ -12,6 +12,8 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 LIB = Path(os.environ.get("SWARM_STAMPS_LIB", ROOT / "build" / "stamps" / "libswarm_stamps.so"))
 NAMES = ["load", "integrate", "pairs+obst", "topk", "reward", "reset", "writeback", "obs"]
+if os.environ.get("SWARM_STAMPS_KERNEL") == "n256":  # swarm_step256's STAMP256 phases (wave 0)
+    NAMES = ["load", "integ+put", "pass1+obst", "handover", "reward", "reset", "keys+finish", "wb+obs"]
 
 if sys.argv[1] == "build":
     LIB.parent.mkdir(parents=True, exist_ok=True)
