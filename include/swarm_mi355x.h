@@ -345,13 +345,17 @@ typedef struct swarm_eval {
   float* goal;            /* [E,N,3] start + obs[6:9] (the reference's goal estimate) */
   float* last;            /* [E,N,3] last observed positions */
   double* traveled;       /* [E,N]   path length */
-  double* records;        /* [capacity, SWARM_EVAL_RECORD] finished episodes; segment s owns rows
-                             [s*C, (s+1)*C), C = capacity / SWARM_EVAL_SEGMENTS */
+  double* records;        /* [capacity, SWARM_EVAL_RECORD] finished episodes; segment s owns the row
+                             block b = (s - seg_base) mod 64 (< segments): rows [b*C, (b+1)*C),
+                             C = capacity / segments */
   uint32_t* count;        /* [SWARM_EVAL_SEGMENTS] records appended per segment (may exceed C: the
                              rest are dropped) */
-  int32_t capacity;       /* a multiple of SWARM_EVAL_SEGMENTS */
+  int32_t capacity;       /* a multiple of `segments` */
   int32_t update_index;   /* stamped into the records this update closes (the caller counts updates) */
   int32_t flags;          /* SWARM_EVAL_STEP_FUSED: the step launches carry this state in out.eval */
+  int32_t seg_base;       /* segment of the tracker's first global env (its env_offset mod 64) */
+  int32_t segments;       /* record segments that receive episodes: min(envs, 64) (0 = 64): a
+                             batch of E < 64 envs holds only E row blocks */
   const float* state_pos;   /* [E,N,3] optional: the env state's positions after the step (bitwise
                                obs[..., 0:3]), read contiguously instead of from the obs rows */
   const float* state_goal;  /* [E,3] optional (with state_pos): the goal; obs[..., 6:9] = goal - pos */

@@ -68,6 +68,17 @@ __device__ __forceinline__ int wave_sum_i(int v) {
   return v;
 }
 
+// Row k of segment seg's record block: block (seg - seg_base) mod 64 of `segments` blocks of
+// capacity / segments rows each; NULL once the block is full (or for a segment outside the
+// tracker's live set, which no env of it maps to)
+__device__ __forceinline__ double* record_slot(const swarm_eval_t& v, unsigned seg, unsigned k) {
+  const unsigned nseg = v.segments > 0 ? (unsigned)v.segments : (unsigned)SWARM_EVAL_SEGMENTS;
+  const unsigned b = (seg + SWARM_EVAL_SEGMENTS - (unsigned)v.seg_base % SWARM_EVAL_SEGMENTS) % SWARM_EVAL_SEGMENTS;
+  const unsigned cap = (unsigned)v.capacity / nseg;
+  if (b >= nseg || k >= cap) return nullptr;
+  return v.records + ((size_t)b * cap + k) * SWARM_EVAL_RECORD;
+}
+
 struct EvalArgs {
   int E, N, D;
   long long env_offset;
@@ -291,10 +302,9 @@ __global__ void __launch_bounds__(EVAL_THREADS * EVAL_WG_ENVS) eval_update_kerne
   const bool collided = coll || (status & SWARM_EVAL_COLLIDED);
   const long long genv = a.env_offset + e;
   const unsigned seg = (unsigned)(genv % SWARM_EVAL_SEGMENTS);
-  const unsigned seg_cap = (unsigned)v.capacity / SWARM_EVAL_SEGMENTS;
   const unsigned k = SWARM_EVAL_ABLATE == 3 ? 0u : atomicAdd(v.count + seg, 1u);
-  if (k < seg_cap) {
-    double* rec = v.records + ((size_t)seg * seg_cap + k) * SWARM_EVAL_RECORD;
+  double* rec = record_slot(v, seg, k);
+  if (rec) {
     rec[0] = (double)genv;  // global env index
     rec[1] = (!collided && reached >= 0) ? 1.0 : 0.0;
     rec[2] = collided ? 0.0 : 1.0;
@@ -347,10 +357,9 @@ __global__ void __launch_bounds__(256) eval_single_update_kernel(const EvalArgs 
                                 v.start[3 * e + 2] - v.goal[3 * e + 2]);
   const long long genv = a.env_offset + e;
   const unsigned seg = (unsigned)(genv % SWARM_EVAL_SEGMENTS);
-  const unsigned seg_cap = (unsigned)v.capacity / SWARM_EVAL_SEGMENTS;
   const unsigned k = atomicAdd(v.count + seg, 1u);
-  if (k < seg_cap) {
-    double* rec = v.records + ((size_t)seg * seg_cap + k) * SWARM_EVAL_RECORD;
+  double* rec = record_slot(v, seg, k);
+  if (rec) {
     rec[0] = (double)genv;
     rec[1] = (!collided && reached >= 0) ? 1.0 : 0.0;
     rec[2] = collided ? 0.0 : 1.0;
@@ -385,8 +394,11 @@ int make_args(const swarm_params_t* p, const swarm_eval_t* ev, const swarm_out_t
   if ((ev->state_pos == nullptr) != (ev->state_goal == nullptr))
     return efail(SWARM_EINVAL, "state_pos and state_goal go together");
   if (ev->flags & ~SWARM_EVAL_STEP_FUSED) return efail(SWARM_EINVAL, "unknown eval flags 0x%x", (unsigned)ev->flags);
-  if (ev->capacity < 0 || ev->capacity % SWARM_EVAL_SEGMENTS != 0)
-    return efail(SWARM_EINVAL, "capacity must be a non-negative multiple of %d", SWARM_EVAL_SEGMENTS);
+  if (ev->segments < 0 || ev->segments > SWARM_EVAL_SEGMENTS || ev->seg_base < 0)
+    return efail(SWARM_EINVAL, "segments must be in [0, %d] and seg_base >= 0", SWARM_EVAL_SEGMENTS);
+  const int nseg = ev->segments > 0 ? ev->segments : SWARM_EVAL_SEGMENTS;
+  if (ev->capacity < 0 || ev->capacity % nseg != 0)
+    return efail(SWARM_EINVAL, "capacity must be a non-negative multiple of segments (%d)", nseg);
   a->E = p->num_envs;
   a->N = p->num_drones;
   a->D = 9 + 4 * (p->neighbor_k > 0 ? p->neighbor_k : 0) + 4 * (p->sensed_obstacles > 0 ? p->sensed_obstacles : 0);

@@ -2629,8 +2629,11 @@ __device__ __forceinline__ void q16_pair_pass(const float* __restrict__ soa, int
   do {                       \
     if (SWARM_LAT_REFETCH_ON) (A) = s64_args(); \
   } while (0)
+#ifndef SWARM_Q16_WAVES_PER_EU
+#define SWARM_Q16_WAVES_PER_EU 8
+#endif
 template <int G>
-__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(8)))
+__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(SWARM_Q16_WAVES_PER_EU)))
 swarm_step16q(const S64Args args) {
   (void)args;  // read through s64_args()
   constexpr int KS = Q_K + 1, MSL = Q_MS + 1;
@@ -3060,6 +3063,9 @@ constexpr int H_BL = 128;       // per-block plane segment: 64 drones + their wr
 #define SWARM_H_BATCH 8
 #endif
 constexpr int H_BATCH = SWARM_H_BATCH;  // rotations per scheduling batch of the pair passes
+#ifndef SWARM_H_SPLIT
+#define SWARM_H_SPLIT 0
+#endif
 
 struct H256Lds {
   // SoA planes per block: seg[b][plane][u], planes x, y, z, eligibility; drone 64b + u at u and
@@ -3283,6 +3289,22 @@ __device__ __forceinline__ void h_pass0(H256Lds& L, int w, int t, float px, floa
   h_bases(L, w, t, A0, A1);
   h_bases(L, b1, t, B0, B1);
   h_bases(L, b2, t, C0, C1);
+#if SWARM_H_SPLIT
+  // two own lists (own block + block w + 2 / block w + 1) and the own block's mirrors in a third:
+  // every rotation feeds two independent insert chains, merged once at the end
+  uint32_t nb[4], km[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) { nb[s] = KEY_EMPTY; km[s] = KEY_EMPTY; }
+  h_seg0<31, 1, 0, 0, true>(A0, A1, t4, px, py, pz, keep, nk, km);
+  h_seg0<32, 32, 0, 0, false>(A0, A1, t4, px, py, pz, keep, nk, km);
+  h_seg0<63, 0, 64, 192, true>(B0, B1, t4, px, py, pz, keep, nb, kb);
+  if (w < 2)
+    h_seg0<31, 0, 128, 128, true>(C0, C1, t4, px, py, pz, keep, nk, kc);
+  else
+    h_seg0<32, 1, 128, 128, true>(C0, C1, t4, px, py, pz, keep, nk, kc);
+  h_merge4(nk, nb);
+  h_merge4(nk, km);
+#else
   h_seg0<31, 1, 0, 0, true>(A0, A1, t4, px, py, pz, keep, nk, nk);
   h_seg0<32, 32, 0, 0, false>(A0, A1, t4, px, py, pz, keep, nk, nk);
   // block (w, w + 1): own code 64 + r (block delta 1); mirror code 192 + (64 - r) % 64 (delta -1)
@@ -3292,6 +3314,7 @@ __device__ __forceinline__ void h_pass0(H256Lds& L, int w, int t, float px, floa
     h_seg0<31, 0, 128, 128, true>(C0, C1, t4, px, py, pz, keep, nk, kc);
   else
     h_seg0<32, 1, 128, 128, true>(C0, C1, t4, px, py, pz, keep, nk, kc);
+#endif
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     L.x.keys[0][s][64 * b1 + t] = kb[s];

@@ -150,7 +150,8 @@ class SwarmEval(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name in
                 ("ep_reward", "ep_steps", "reached_step", "status", "fe_sum", "start", "goal", "last",
                  "traveled", "records", "count")] + [("capacity", ctypes.c_int32), ("update_index", ctypes.c_int32),
-                                                     ("flags", ctypes.c_int32),
+                                                     ("flags", ctypes.c_int32), ("seg_base", ctypes.c_int32),
+                                                     ("segments", ctypes.c_int32),
                                                      ("state_pos", ctypes.c_void_p), ("state_goal", ctypes.c_void_p)]
 
 

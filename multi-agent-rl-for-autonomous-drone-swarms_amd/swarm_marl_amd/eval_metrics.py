@@ -78,14 +78,16 @@ class EvalTracker:
         self.last = torch.zeros_like(self.start)
         self.traveled = torch.zeros((e, n), **f64)
         seg = nat.EVAL_SEGMENTS
-        # segment s holds the episodes of global envs g with g % 64 == s, so only min(E, 64)
-        # segments are ever written and the busiest holds ceil(E / 64) envs: size every segment
-        # for that one's share of `capacity` episodes (capacity * ceil(E/64) / E), so that
-        # `capacity` finished episodes fit whatever E is (E = 8: 8 live segments, not 64)
-        seg_cap = max(1, -(-int(capacity) * (-(-e // seg)) // e))
-        self.capacity = seg * seg_cap
+        # segment s holds the episodes of global envs g with g % 64 == s: only min(E, 64) segments
+        # are ever written (row blocks (s - seg_base) mod 64 < segments) and the busiest holds
+        # ceil(E / 64) envs — every live block is sized for that one's share of `capacity`
+        # episodes (capacity * ceil(E/64) / E), so `capacity` finished episodes fit whatever E is
+        self.segments = min(e, seg) if e > 0 else seg
+        seg_cap = max(1, -(-int(capacity) * (-(-e // seg)) // max(e, 1)))
+        self.capacity = self.segments * seg_cap
         self.records_buf = torch.zeros((self.capacity, nat.EVAL_RECORD), **f64)
         self.count = torch.zeros(seg, dtype=torch.int32, device=dev)
+        self.seg_base = int(vec.params.env_offset) % seg
         self.updates = 0
         c = nat.SwarmEval()
         for name in ("ep_reward", "ep_steps", "reached_step", "status", "fe_sum", "start", "goal", "last",
@@ -93,6 +95,7 @@ class EvalTracker:
             setattr(c, name, getattr(self, name).data_ptr())
         c.records = self.records_buf.data_ptr()
         c.capacity = self.capacity
+        c.seg_base, c.segments = self.seg_base, self.segments
         # positions / goal from the state tensors (contiguous) rather than the strided obs rows
         c.state_pos, c.state_goal = vec.pos.data_ptr(), vec.goal.data_ptr()
         self._c = c
@@ -175,7 +178,7 @@ class EvalTracker:
             setattr(c, name, t.data_ptr() + lo * t.stride(0) * t.element_size())
         c.records, c.count, c.capacity = self.records_buf.data_ptr(), self.count.data_ptr(), self.capacity
         c.update_index = self.updates
-        c.flags = self._c.flags
+        c.flags, c.seg_base, c.segments = self._c.flags, self.seg_base, self.segments
         v = self.vec
         c.state_pos = v.pos.data_ptr() + lo * v.pos.stride(0) * v.pos.element_size()
         c.state_goal = v.goal.data_ptr() + lo * v.goal.stride(0) * v.goal.element_size()
@@ -184,18 +187,23 @@ class EvalTracker:
     def overflowed(self) -> bool:
         """True once a record segment has filled (further episodes of its envs are dropped by
         the kernel): one 256-B device read, for long runs to check every few thousand updates."""
-        return int(self.count.max()) > self.capacity // nat.EVAL_SEGMENTS
+        return int(self.count.max()) > self.capacity // self.segments
 
     def records(self) -> np.ndarray:
         """Finished-episode records [n, 9] (FIELDS), in completion order: by the update that
         closed them, then by global env index (deterministic)."""
         counts = self.count.cpu().numpy().astype(np.int64)
-        seg_cap = self.capacity // nat.EVAL_SEGMENTS
+        seg_cap = self.capacity // self.segments
         if counts.max(initial=0) > seg_cap:
             raise RuntimeError(f"{int(counts.max())} episodes finished in one record segment, which holds "
                                f"{seg_cap} (EvalTracker capacity {self.capacity}); raise the capacity")
         buf = self.records_buf.cpu().numpy()
-        rec = np.concatenate([buf[s * seg_cap:s * seg_cap + int(c)] for s, c in enumerate(counts)], axis=0)
+        blocks = []
+        for s, c in enumerate(counts):
+            if c:
+                b = (s - self.seg_base) % nat.EVAL_SEGMENTS  # < segments for every written segment
+                blocks.append(buf[b * seg_cap:b * seg_cap + int(c)])
+        rec = np.concatenate(blocks, axis=0) if blocks else np.zeros((0, nat.EVAL_RECORD))
         return rec[np.lexsort((rec[:, 0], rec[:, 8]))]
 
     def aggregate(self) -> dict:

@@ -151,6 +151,26 @@ def test_fused_eval_equals_unfused(dev, groups, native):
     assert np.array_equal(a, b, equal_nan=True)
 
 
+def test_record_blocks_only_for_live_segments(dev):
+    """E < 64 envs write min(E, 64) record segments: only those blocks are allocated (ADVICE r03:
+    E = 1 at the default capacity took 64 blocks, ~302 MB), also at an env_offset that wraps
+    the segment ring."""
+    from swarm_marl_amd import VecSwarm
+    from swarm_marl_amd.eval_metrics import EvalTracker
+    vec = VecSwarm(3, {"num_drones": 4, "max_steps": 5}, device=dev, auto_reset=True, with_infos=True,
+                   env_offset=126)  # global envs 126, 127, 128: segments 62, 63, 0
+    vec.reset()
+    ev = EvalTracker(vec, capacity=90)
+    assert ev.segments == 3 and ev.seg_base == 62 and ev.records_buf.shape[0] == 90
+    ev.begin()
+    for _ in range(26):
+        vec.step(torch.zeros((3, 4, 3), device=dev))
+        ev.update()
+    rec = ev.records()
+    assert sorted(set(rec[:, 0].astype(int))) == [126, 127, 128]
+    assert len(rec) >= 15 and np.all(rec[:, 7] <= 5)  # episodes end by the 5-step time limit or earlier
+
+
 def test_fused_eval_needs_step64(dev):
     """out.eval on a launch other than the kinematic step64 one is refused (SWARM_EINVAL)."""
     from swarm_marl_amd import VecSwarm
