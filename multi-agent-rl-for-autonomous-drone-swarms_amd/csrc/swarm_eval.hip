@@ -256,12 +256,21 @@ __global__ void __launch_bounds__(EVAL_THREADS * EVAL_WG_ENVS) eval_update_kerne
     // is not reproduced: 1e-9 relative).
     const float4 p = pos[t];
     double s_a = 0.0, s_b = 0.0;  // two chains of dependent f64 adds instead of one
+    if (n_obs == EVAL_THREADS) {  // every drone observed (the common step): no pair masks
 #pragma unroll 8
-    for (int r = 1; r < 32; ++r) {
-      const float4 q = pos[(t + r) & (EVAL_THREADS - 1)];
-      const float d = norm1d_fast(p.x - q.x, p.y - q.y, p.z - q.z);
-      const double term = (p.w != 0.f && q.w != 0.f) ? fabs((double)d - a.spacing) : 0.0;
-      if (r & 1) s_a += term; else s_b += term;
+      for (int r = 1; r < 32; ++r) {
+        const float4 q = pos[(t + r) & (EVAL_THREADS - 1)];
+        const double term = fabs((double)norm1d_fast(p.x - q.x, p.y - q.y, p.z - q.z) - a.spacing);
+        if (r & 1) s_a += term; else s_b += term;
+      }
+    } else {
+#pragma unroll 8
+      for (int r = 1; r < 32; ++r) {
+        const float4 q = pos[(t + r) & (EVAL_THREADS - 1)];
+        const float d = norm1d_fast(p.x - q.x, p.y - q.y, p.z - q.z);
+        const double term = (p.w != 0.f && q.w != 0.f) ? fabs((double)d - a.spacing) : 0.0;
+        if (r & 1) s_a += term; else s_b += term;
+      }
     }
     const float4 q = pos[(t + 32) & (EVAL_THREADS - 1)];
     const float d = norm1d_fast(p.x - q.x, p.y - q.y, p.z - q.z);
