@@ -463,9 +463,15 @@ typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
 typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr float X3_LO_SCALE = 2048.f, X3_LO_INV = 1.f / 2048.f;
 #ifndef SWARM_POLICY_X3_BATCH
-#define SWARM_POLICY_X3_BATCH 8
+#define SWARM_POLICY_X3_BATCH 4
 #endif
 constexpr int X3_B = SWARM_POLICY_X3_BATCH;  // W2 k-steps per lo-fragment batch (divides 16)
+#ifndef SWARM_POLICY_X3_EARLY_W3
+#define SWARM_POLICY_X3_EARLY_W3 1
+#endif
+// layer-3 lo fragments requested at the top of their out block (fits the 512 registers with
+// 4-k-step W2 batches; with 8-step batches it spills)
+constexpr bool X3_EARLY_W3 = SWARM_POLICY_X3_EARLY_W3 != 0;
 
 // 8 accumulator values (sub-block s) -> hi / lo f16 fragments, relu'd first when `act`
 __device__ __forceinline__ void split8(const f32x16& a, int s, bool act, f16x8& hi, f16x8& lo) {
@@ -612,6 +618,13 @@ policy_mlp_x3(const FwdArgs A) {
         const float4 b = *reinterpret_cast<const float4*>(b2 + ob * 32 + 8 * g + 4 * h);
         acc[4 * g + 0] = b.x; acc[4 * g + 1] = b.y; acc[4 * g + 2] = b.z; acc[4 * g + 3] = b.w;
       }
+      // this block's layer-3 lo fragments (k-steps 2ob, 2ob+1): requested a whole block ahead of use
+      // (one wave per SIMD: nothing else hides the L2 round trip)
+      f16x8 a0l = {}, a1l = {};
+      if (X3_EARLY_W3 && w3lane) {
+        a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob) * 2 * out * 16));
+        a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob + 1) * 2 * out * 16));
+      }
 #pragma unroll
       for (int kb = 0; kb < KS2; kb += X3_B) {
         const int bi = (ob * KS2 + kb) / X3_B;  // batch index
@@ -628,12 +641,14 @@ policy_mlp_x3(const FwdArgs A) {
         __builtin_amdgcn_sched_barrier(0);
       }
       acc = x3_sum(acc, accx, accy);
-      f16x8 a0h = {}, a1h = {}, a0l = {}, a1l = {};
+      f16x8 a0h = {}, a1h = {};
       if (w3lane) {
         a0h = w3f[(2 * ob) * 2 * out + w3idx];
         a1h = w3f[(2 * ob + 1) * 2 * out + w3idx];
-        a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob) * 2 * out * 16));
-        a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob + 1) * 2 * out * 16));
+        if (!X3_EARLY_W3) {
+          a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob) * 2 * out * 16));
+          a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob + 1) * 2 * out * 16));
+        }
       }
       f16x8 h2h, h2l;
       split8(acc, 0, true, h2h, h2l);
