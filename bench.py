@@ -386,7 +386,8 @@ def main(argv=None):
 
     # plain env steps with groups: one native call launches every group on its stream
     # (swarm_step_groups), instead of a Python stream context + launch per group
-    native_groups = G > 1 and pol is None and tracker is None and not args.split_reset
+    # (a fused eval tracker needs no launch of its own: the step launches update it)
+    native_groups = G > 1 and pol is None and (tracker is None or tracker.fused) and not args.split_reset
 
     def env_step(k):  # whole batch: group g on group stream g (not joined: groups overlap)
         if G == 1:
@@ -394,6 +395,8 @@ def main(argv=None):
             return
         if native_groups:
             vec.step_groups(ring[k % args.ring])
+            if tracker is not None:
+                tracker.update()
             return
         for g, st in enumerate(vec.group_streams):
             with torch.cuda.stream(st):
@@ -744,9 +747,11 @@ def main(argv=None):
                              "weights": "random-init TorchFC [256, 256] relu (no checkpoint)"}
             rec["roofline"]["note"] = "env-step roofline fields cover the whole rollout step"
         if tracker is not None:
-            rec["eval"] = {"tracker": "EvalTracker: swarm_eval_update per env group after its step (episode "
-                                      "reward, path length, exact formation error, votes, records)",
-                           "updates": tracker.updates}
+            rec["eval"] = {"tracker": ("EvalTracker fused into the step launches (swarm_step64_eval_once: episode "
+                                       "reward, path length, exact formation error, votes, records)" if tracker.fused else
+                                       "EvalTracker: swarm_eval_update per env group after its step (episode "
+                                       "reward, path length, exact formation error, votes, records)"),
+                           "fused": tracker.fused, "updates": tracker.updates}
         if not args.no_cpu_baseline and world == 1:
             rec["cpu_baseline"] = cpu_baseline_port(n, e, args.cpu_seconds, raw, args.dynamics == "physics")
             if args.cpu_variant_seconds > 0 and not args.no_term and args.dynamics == "kinematic":

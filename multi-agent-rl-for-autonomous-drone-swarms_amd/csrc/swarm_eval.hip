@@ -446,6 +446,8 @@ int swarm_eval_update(const swarm_params_t* p, const swarm_eval_t* ev, const swa
   if (!o->reward || !o->info_flags || !o->env_done)
     return efail(SWARM_ENULL, "out.reward/info_flags/env_done required (build the env with infos)");
   if (a.E == 0) return SWARM_OK;
+  // SWARM_EVAL_STEP_FUSED: the step launches (out.eval) did this update's work already
+  if (ev->flags & SWARM_EVAL_STEP_FUSED) return SWARM_OK;
   hipLaunchKernelGGL(eval_update_kernel, dim3((a.E + EVAL_WG_ENVS - 1) / EVAL_WG_ENVS), dim3(EVAL_THREADS * EVAL_WG_ENVS),
                      (unsigned)(EVAL_WG_ENVS * a.N * sizeof(float4)),
                      (hipStream_t)hip_stream, a);

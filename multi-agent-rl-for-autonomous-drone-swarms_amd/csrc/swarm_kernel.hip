@@ -160,6 +160,17 @@ __device__ __forceinline__ float sqrt_rn(float x) {
   r = (ep > 0.0f) ? rp : r;
   return r;
 }
+// sqrt_rn's fast path alone, for branch-free loops: `tiny` records an input below 2^-96 (the
+// caller redoes the loop with sqrt_rn when any lane saw one; the value returned then is unused)
+__device__ __forceinline__ float sqrt_rn_nb(float x, bool& tiny) {
+  tiny = tiny | !(x >= 0x1p-96f || x == 0.0f);
+  float r = __builtin_amdgcn_sqrtf(x);
+  const float rm = __uint_as_float(__float_as_uint(r) - 1u), rp = __uint_as_float(__float_as_uint(r) + 1u);
+  const float em = __builtin_fmaf(-rm, r, x), ep = __builtin_fmaf(-rp, r, x);
+  r = (em <= 0.0f) ? rm : r;
+  r = (ep > 0.0f) ? rp : r;
+  return r;
+}
 __device__ __forceinline__ double dsqrt_rn(double x) { return __builtin_sqrt(x); }
 // np.linalg.norm(v) of a float32 3-vector: OpenBLAS sdot = double accumulation of float
 // products, rounded to float.  Returns the float sum s; the norm is sqrt_rn(s).
@@ -1716,12 +1727,25 @@ struct S64In {
 // spill them; scalar-cache hits cost a few cycles).
 // The eval tracker's per-step accumulators (swarm_out_t.eval, SWARM_EVAL_STEP_FUSED): device
 // pointers of this launch's env rows, NULL status = off.
+// A wave-uniform double (after a full butterfly) into SGPRs
+__device__ __forceinline__ double s64_uniform(double v) {
+  const uint64_t u = __double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 struct S64Eval {
   double* ep_reward;
   int32_t* ep_steps;
   int32_t* reached_step;
   uint8_t* status;
   double* traveled;
+  double* fe_sum;
+  float* start;        // [E,N,3] episode start positions
+  float* goal;         // [E,N,3] the protocol's goal estimate, start + obs[6:9]
+  double* records;     // swarm_eval_t.records / count / capacity / update_index / seg_base / segments
+  uint32_t* count;
+  int32_t capacity, update_index, seg_base, segments;
+  double spacing;      // DroneEnvConfig.desired_spacing (the formation error's d*)
 };
 struct S64Args {
   KParams P;
@@ -1773,7 +1797,7 @@ __device__ __forceinline__ void s64_load(S64ArgPtr A, int env, int t, S64In& c) 
 // LANDED: wait for them (and the queue ticket) after the pair pass, before this env issues any
 // store — vmcnt counts loads and stores in order, so a wait left to the next env's first use would
 // also wait for this env's stores.
-template <int CH, bool LANDED, class Prefetch, int DYN = DYN_KIN>
+template <int CH, bool LANDED, class Prefetch, int DYN = DYN_KIN, bool EVAL = false>
 __device__ __forceinline__ void s64_env(const int env, const int M, const S64In& c, float4* __restrict__ ring,
                                         float4* __restrict__ obst, float* __restrict__ stage, const int lane,
                                         Prefetch&& prefetch) {
@@ -2079,17 +2103,20 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     A->O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
                                 (do_reset ? SWARM_ENV_RESET : 0u));
   const uint64_t m_term = __ballot(term), m_trunc = __ballot(trunc);
-  if (DYN == DYN_KIN && A->EV.status != nullptr) {
-    // fused eval: swarm_eval_update's per-step part (swarm_eval.hip eval_update_kernel, the same
-    // arithmetic and f64 butterfly): episode reward += mean reward of the stepped agents, steps,
-    // the first step all observed agents reached, the collision vote, path lengths
+  bool ev_restart = false;  // fused eval: a live episode ended here and the env restarts
+  if constexpr (EVAL) __builtin_amdgcn_sched_barrier(0);  // the finish's reads stay below the eval block
+  if (EVAL && DYN == DYN_KIN && A->EV.status != nullptr) {
+    // fused eval (out.eval, SWARM_EVAL_STEP_FUSED): everything swarm_eval_update does for one step
+    // (swarm_eval.hip eval_update_kernel: the same arithmetic, the same f64 butterflies), with the
+    // positions already in registers / LDS: episode reward += mean reward of the stepped agents,
+    // steps, the first step all observed agents reached, the collision vote, path lengths, the
+    // exact formation error of the observed drones, and at an episode's end its record
     const uint8_t status = A->EV.status[env];
     if (status & SWARM_EVAL_LIVE) {
-      double rsum = (double)rew;  // 0 for agents without a reward entry
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) rsum += __shfl_xor(rsum, o);
       const bool coll = __ballot(cont && collided) != 0;
       const bool not_reached = __ballot(cont && !reached) != 0;
+      const uint64_t m_obs = __ballot(cont);
+      const int n_obs = __popcll(m_obs);
       if (cont) {
         // path length += |last - p| (evaluate_protocol.py's _distance: the sdot-double norm); last =
         // the position this step started from, still in the state (written back below): an agent
@@ -2099,17 +2126,110 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
         double* tr = A->EV.traveled + ea + t;
         *tr = *tr + (double)inc;
       }
+      // formation error (evaluate_protocol.py:103-116) of the observed drones: symmetric lane
+      // rotations over the pair-pass ring (the emitted positions), each pair measured once,
+      // 2 S_{r<32} + S_32 over n (n - 1) (eval_update_kernel's order, term for term); the wave
+      // sums end uniform and are moved to SGPRs at once (short VGPR live ranges: the kernel runs
+      // at 64 VGPRs)
+      double fe = 0.0;
+      if (n_obs > 1) {
+        const double sp = A->EV.spacing;
+        const bool all = n_obs == S64_N;
+        // one pass: the square roots without sqrt_rn's per-call slow-path branch (a branch per
+        // pair splits the loop into blocks the register allocator spills across); a coincident
+        // pair (s' < 2^-96) on any lane redoes the pass with sqrt_rn, bit for bit the same terms
+        auto pass = [&](auto sqrt_fn) -> double {
+          // opaque ring base per pass: the two passes' reads must not be merged (96 values
+          // would then stay live from the first pass into the second)
+          const float* s0 = soa + t;
+          asm volatile("" : "+v"(s0));
+          double s_a = 0.0, s_b = 0.0;  // odd / even rotations (eval_update_kernel's two chains)
+          auto term = [&](int r) -> double {
+            const float d = sqrt_fn(sqsum_1d(px - s0[r], py - s0[S64_SOA + r], pz - s0[2 * S64_SOA + r]));
+            const bool both = all || (cont && ((m_obs >> ((t + r) & (S64_N - 1))) & 1ull));
+            return both ? fabs((double)d - sp) : 0.0;
+          };
+          // a rolled loop of two rotations: unrolled, the scheduler computes every term up front
+          // and keeps them live for the in-order f64 sums (spills at 64 VGPRs)
+#pragma unroll 1
+          for (int r = 1; r < 31; r += 2) {
+            s_a += term(r);
+            s_b += term(r + 1);
+          }
+          s_a += term(31);
+          const float d32 = sqrt_fn(sqsum_1d(px - s0[32], py - s0[S64_SOA + 32], pz - s0[2 * S64_SOA + 32]));
+          const bool both32 = cont && ((m_obs >> ((t + 32) & (S64_N - 1))) & 1ull);
+          return 2.0 * (s_a + s_b) + (both32 ? fabs((double)d32 - sp) : 0.0);
+        };
+        bool tiny = false;
+        double v = pass([&](float x) { return sqrt_rn_nb(x, tiny); });
+        if (__ballot(tiny) != 0) v = pass([](float x) { return sqrt_rn(x); });
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        fe = s64_uniform(v) / ((double)n_obs * (double)(n_obs - 1));
+      }
+      const bool ends = term_all || trunc_all;
+      // path efficiency of an ending episode: mean over agents of |start - goal| / path length
+      double pe = 0.0;
+      if (ends) {
+        const float* st0 = A->EV.start + (ea + t) * 3;
+        const float* gl0 = A->EV.goal + (ea + t) * 3;
+        const double tr = A->EV.traveled[ea + t];
+        const float straight = sqrt_rn(sqsum_1d(st0[0] - gl0[0], st0[1] - gl0[1], st0[2] - gl0[2]));
+        double q = tr > 1e-8 ? (double)straight / tr : 0.0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+        pe = s64_uniform(q) / (double)S64_N;
+      }
+      double rsum = (double)rew;  // 0 for agents without a reward entry
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) rsum += __shfl_xor(rsum, o);
+      rsum = s64_uniform(rsum);
       if (t == 0) {
         const int steps = A->EV.ep_steps[env] + 1;
         int rs = A->EV.reached_step[env];
         if (!not_reached && rs < 0) rs = steps;
-        A->EV.ep_reward[env] = A->EV.ep_reward[env] + (n_active > 0 ? rsum / (double)n_active : 0.0);
-        A->EV.ep_steps[env] = steps;
-        A->EV.reached_step[env] = rs;
-        if (coll) A->EV.status[env] = (uint8_t)(status | SWARM_EVAL_COLLIDED);
+        const double ep_reward = A->EV.ep_reward[env] + (n_active > 0 ? rsum / (double)n_active : 0.0);
+        const double fe_sum = A->EV.fe_sum[env] + fe;
+        if (!ends) {
+          A->EV.ep_reward[env] = ep_reward;
+          A->EV.fe_sum[env] = fe_sum;
+          A->EV.ep_steps[env] = steps;
+          A->EV.reached_step[env] = rs;
+          if (coll) A->EV.status[env] = (uint8_t)(status | SWARM_EVAL_COLLIDED);
+        } else {
+          // one record {env, success, collision-free, TTG, FE, PE, reward, steps, update}
+          const bool coll_ep = coll || (status & SWARM_EVAL_COLLIDED);
+          const long long genv = A->P.env_offset + env;
+          const unsigned seg = (unsigned)(genv % SWARM_EVAL_SEGMENTS);
+          const unsigned k = atomicAdd(A->EV.count + seg, 1u);
+          const unsigned nseg = A->EV.segments > 0 ? (unsigned)A->EV.segments : (unsigned)SWARM_EVAL_SEGMENTS;
+          const unsigned b = (seg + SWARM_EVAL_SEGMENTS - (unsigned)A->EV.seg_base % SWARM_EVAL_SEGMENTS) %
+                             SWARM_EVAL_SEGMENTS;
+          const unsigned cap = (unsigned)A->EV.capacity / nseg;
+          if (b < nseg && k < cap) {
+            double* rec = A->EV.records + ((size_t)b * cap + k) * SWARM_EVAL_RECORD;
+            rec[0] = (double)genv;
+            rec[1] = (!coll_ep && rs >= 0) ? 1.0 : 0.0;
+            rec[2] = coll_ep ? 0.0 : 1.0;
+            rec[3] = rs >= 0 ? (double)rs : __builtin_nan("");
+            rec[4] = fe_sum / (double)steps;
+            rec[5] = pe;
+            rec[6] = ep_reward;
+            rec[7] = (double)steps;
+            rec[8] = (double)A->EV.update_index;
+          }
+          A->EV.ep_reward[env] = 0.0;
+          A->EV.fe_sum[env] = 0.0;
+          A->EV.ep_steps[env] = 0;
+          A->EV.reached_step[env] = -1;
+          A->EV.status[env] = do_reset ? (uint8_t)SWARM_EVAL_LIVE : (uint8_t)0;
+        }
       }
+      ev_restart = ends && do_reset;
     }
   }
+  if constexpr (EVAL) __builtin_amdgcn_sched_barrier(0);
   STAMP_AT(srec, 5);
   A = s64_args();
 
@@ -2210,6 +2330,15 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     gs[t3] = px; gs[t3 + 1] = py; gs[t3 + 2] = pz;
     gs[3 * S64_N + t3] = vx; gs[3 * S64_N + t3 + 1] = vy; gs[3 * S64_N + t3 + 2] = vz;
     if (t == 0) { gs[6 * S64_N + 0] = gx; gs[6 * S64_N + 1] = gy; gs[6 * S64_N + 2] = gz; }
+  }
+  if (EVAL && DYN == DYN_KIN && ev_restart) {
+    // fused eval: the next episode opens from its first observation (eval_update_kernel's
+    // restart: start = p, goal = p + obs[6:9] = p + (g - p), path length 0)
+    float* st0 = A->EV.start + (ea + t) * 3;
+    float* gl0 = A->EV.goal + (ea + t) * 3;
+    st0[0] = px; st0[1] = py; st0[2] = pz;
+    gl0[0] = px + (gx - px); gl0[1] = py + (gy - py); gl0[2] = pz + (gz - pz);
+    A->EV.traveled[ea + t] = 0.0;
   }
 
   STAMP_AT(srec, 7);
@@ -2361,7 +2490,7 @@ __device__ __forceinline__ void s64_set_priority() {
 #endif
 constexpr int S64_WG_ENVS = SWARM_S64_WG_ENVS;
 // The body of both one-wave-per-env kernels (kinematic / physics).
-template <int CH, int G, int DYN>
+template <int CH, int G, int DYN, bool EVAL = false>
 __device__ __forceinline__ void s64_once_body() {
   __shared__ S64Lds<CH> lds[G];
   s64_set_priority();
@@ -2372,7 +2501,7 @@ __device__ __forceinline__ void s64_once_body() {
   if (env >= s64_args()->P.E) return;  // whole wave (the last workgroup of a ragged E)
   S64In cur;
   s64_load<DYN>(s64_args(), env, t, cur);
-  s64_env<CH, false, void (*)(), DYN>(env, s64_args()->P.M, cur, lds[w].w.ring, lds[w].w.obst,
+  s64_env<CH, false, void (*)(), DYN, EVAL>(env, s64_args()->P.M, cur, lds[w].w.ring, lds[w].w.obst,
                                       reinterpret_cast<float*>(lds[w].stage), t, []() {});
 }
 template <int CH, int G>
@@ -2385,6 +2514,17 @@ swarm_step64_once(const S64Args args) {
 // same rings, passes, finish and obs staging, with the substep integrate, s' keys, contact
 // thresholds, physics rewards / terminations, reset ranges and the clamped obs velocity of
 // swarm_kernel<0, DYN_PHYS, 4, 5, 2>, bit for bit.
+// The headline step with the evaluation protocol fused in (out.eval, SWARM_EVAL_STEP_FUSED):
+// a separate instantiation, so the plain step's registers and schedule are untouched.
+#ifndef SWARM_S64_EVAL_WAVES
+#define SWARM_S64_EVAL_WAVES 8
+#endif
+template <int CH, int G>
+__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(SWARM_S64_EVAL_WAVES)))
+swarm_step64_eval_once(const S64Args args) {
+  (void)args;
+  s64_once_body<CH, G, DYN_KIN, true>();
+}
 template <int CH, int G>
 __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(8)))
 swarm_step64_phys_once(const S64Args args) {
@@ -2629,8 +2769,10 @@ __device__ __forceinline__ void q16_pair_pass(const float* __restrict__ soa, int
   do {                       \
     if (SWARM_LAT_REFETCH_ON) (A) = s64_args(); \
   } while (0)
+// 71 VGPRs without spills at 4 waves per EU (at 8: 64 VGPRs and 4 spilled, scratch round trips
+// on a latency-bound launch): config 2 (one wave per SIMD) 6.58 vs 6.85 us per step
 #ifndef SWARM_Q16_WAVES_PER_EU
-#define SWARM_Q16_WAVES_PER_EU 8
+#define SWARM_Q16_WAVES_PER_EU 4
 #endif
 template <int G>
 __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(SWARM_Q16_WAVES_PER_EU)))
@@ -3703,6 +3845,7 @@ SWARM_PICK_DECL(2);
 SWARM_PICK_DECL(3);
 // the headline specialisation (SWARM_PART 5)
 __attribute__((visibility("hidden"))) void* swarm_pick_step64(bool persistent, bool physics);
+__attribute__((visibility("hidden"))) void* swarm_pick_step64_eval();
 // the config-2 specialisation (SWARM_PART 6)
 __attribute__((visibility("hidden"))) void* swarm_pick_step16q();
 // the config-5 specialisation (SWARM_PART 7)
@@ -3716,6 +3859,9 @@ __attribute__((visibility("hidden"))) void* swarm_pick_step16q() {
 }
 #endif
 #if SWARM_HAS_PART(5)
+__attribute__((visibility("hidden"))) void* swarm_pick_step64_eval() {
+  return reinterpret_cast<void*>(swarm_step64_eval_once<S64_CH, S64_WG_ENVS>);
+}
 __attribute__((visibility("hidden"))) void* swarm_pick_step64(bool persistent, bool physics) {
   if (physics) return reinterpret_cast<void*>(swarm_step64_phys_once<S64_CH, S64_WG_ENVS>);
   return persistent ? reinterpret_cast<void*>(swarm_step64<S64_CH>)
@@ -3974,7 +4120,7 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   // ballot-packed byte outputs need N == 64 and dword-aligned bool tensors
   kp.pack_bytes = (kp.N == 64 && mode == MODE_STEP && ((uintptr_t)o->terminated | (uintptr_t)o->truncated |
                                                        (uintptr_t)s->active) % 4 == 0) ? 1 : 0;
-  S64Eval ev{nullptr, nullptr, nullptr, nullptr, nullptr};
+  S64Eval ev{};
   if (o->eval) {
     // fused eval accumulation: the kinematic one-wave-per-env step64 launch only
     const swarm_eval_t* e = o->eval;
@@ -3984,10 +4130,15 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
       return fail(SWARM_EINVAL, "out.eval (fused eval accumulation) needs the kinematic swarm_step64 launch "
                                 "(N = 64, K = 3, Ms = 4, no env_cfg, no persistent grid)");
     if (!(e->flags & SWARM_EVAL_STEP_FUSED)) return fail(SWARM_EINVAL, "out.eval without SWARM_EVAL_STEP_FUSED in its flags");
-    if (!e->ep_reward || !e->ep_steps || !e->reached_step || !e->status || !e->traveled)
-      return fail(SWARM_ENULL, "out.eval: an accumulator buffer is NULL");
-    if (!o->info_flags) return fail(SWARM_ENULL, "out.eval needs out.info_flags (swarm_eval_update reads them)");
-    ev = S64Eval{e->ep_reward, e->ep_steps, e->reached_step, e->status, e->traveled};
+    if (!e->ep_reward || !e->ep_steps || !e->reached_step || !e->status || !e->traveled || !e->fe_sum || !e->start ||
+        !e->goal || !e->records || !e->count)
+      return fail(SWARM_ENULL, "out.eval: an eval state buffer is NULL");
+    const int nseg = e->segments > 0 ? e->segments : SWARM_EVAL_SEGMENTS;
+    if (e->segments < 0 || e->segments > SWARM_EVAL_SEGMENTS || e->seg_base < 0 || e->capacity < 0 ||
+        e->capacity % nseg != 0)
+      return fail(SWARM_EINVAL, "out.eval: bad capacity / segments / seg_base");
+    ev = S64Eval{e->ep_reward, e->ep_steps, e->reached_step, e->status, e->traveled, e->fe_sum, e->start, e->goal,
+                 e->records, e->count, e->capacity, e->update_index, e->seg_base, e->segments, p->desired_spacing};
   }
   if (mode == MODE_STEP && step64_applies(p, kp) && kp.obs_vec4 && kp.pack_bytes && !s->env_cfg) {
     swarm_state_t st = *s;
@@ -3999,7 +4150,7 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
       hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step64(true, false)), dim3(grid), dim3(64), 0,
                          (hipStream_t)stream, args);
     else
-      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step64(false, phys)),
+      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(ev.status ? swarm_pick_step64_eval() : swarm_pick_step64(false, phys)),
                          dim3((kp.E + S64_WG_ENVS - 1) / S64_WG_ENVS), dim3(64 * S64_WG_ENVS), 0, (hipStream_t)stream,
                          args);
     hipError_t e = hipGetLastError();
@@ -4244,6 +4395,10 @@ int swarm_step_groups(const swarm_params_t* p, const swarm_state_t* s, const flo
       eg.reached_step = row(eg.reached_step, 1);
       eg.status = row(eg.status, 1);
       eg.traveled = row(eg.traveled, N);
+      eg.fe_sum = row(eg.fe_sum, 1);
+      eg.start = row(eg.start, 3 * N);
+      eg.goal = row(eg.goal, 3 * N);
+      eg.last = row(eg.last, 3 * N);
       og.eval = &eg;
     }
     og.obs = row(o->obs, N * D);

@@ -463,14 +463,15 @@ typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
 typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr float X3_LO_SCALE = 2048.f, X3_LO_INV = 1.f / 2048.f;
 #ifndef SWARM_POLICY_X3_BATCH
-#define SWARM_POLICY_X3_BATCH 4
+#define SWARM_POLICY_X3_BATCH 8
 #endif
 constexpr int X3_B = SWARM_POLICY_X3_BATCH;  // W2 k-steps per lo-fragment batch (divides 16)
 #ifndef SWARM_POLICY_X3_EARLY_W3
-#define SWARM_POLICY_X3_EARLY_W3 1
+#define SWARM_POLICY_X3_EARLY_W3 0
 #endif
-// layer-3 lo fragments requested at the top of their out block (fits the 512 registers with
-// 4-k-step W2 batches; with 8-step batches it spills)
+// layer-3 lo fragments requested at the top of their out block (fits the 512 registers only
+// with 4-k-step W2 batches, and measured slower that way: 322.8 / 328.6 vs 314-315 us per rollout
+// step for 8-step batches with the fragments requested at their use, profiles/r04c_lines.txt)
 constexpr bool X3_EARLY_W3 = SWARM_POLICY_X3_EARLY_W3 != 0;
 
 // 8 accumulator values (sub-block s) -> hi / lo f16 fragments, relu'd first when `act`

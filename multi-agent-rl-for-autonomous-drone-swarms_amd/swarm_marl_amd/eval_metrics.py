@@ -53,11 +53,13 @@ def aggregate_records(rec: np.ndarray) -> dict:
 
 class EvalTracker:
     """fused (default "auto"): where the step runs the kinematic swarm_step64 kernel (N = 64,
-    K = 3, Ms = 4, no per-env records), the step itself accumulates the per-step terms in its
-    write-back (out.eval, SWARM_EVAL_STEP_FUSED: episode reward, steps, reached step, collision
-    vote, path length) and update() adds only the formation error and closes ended episodes —
-    same records (tests/test_gpu_eval.py).  Every step of the VecSwarm then accumulates, so
-    update() must follow every step (as without fusion); `detach()` ends the fusion."""
+    K = 3, Ms = 4, no per-env records), the step itself does the whole update (out.eval,
+    SWARM_EVAL_STEP_FUSED: swarm_step64_eval_once adds the episode reward, steps, reached step,
+    collision vote, path lengths and the exact formation error, and writes the record of every
+    episode that ends) — the same records, bit for bit (tests/test_gpu_eval.py) — and update()
+    launches nothing: it counts the update (the record's update index).  Every step of the
+    VecSwarm then updates, so call update() after every step (as without fusion); `detach()`
+    ends the fusion."""
 
     def __init__(self, vec: VecSwarm, capacity: int = 65536, fused="auto"):
         if vec.info_flags is None:
@@ -119,6 +121,7 @@ class EvalTracker:
         for g, sc in enumerate(self._step_c):
             sc.flags = nat.EVAL_STEP_FUSED
             vec._gout[g].eval = ctypes.addressof(sc)
+        self._next_index()
         vec._eval_owner = self  # the structs and tensors stay alive while the VecSwarm writes them
 
     def detach(self) -> None:
@@ -147,8 +150,17 @@ class EvalTracker:
                                                 ctypes.byref(self.vec._gout[g]), None if mp is None else mp + lo,
                                                 self._stream()), self.lib, which="eval")
 
+    def _next_index(self) -> None:
+        """The update index the next fused step stamps into the records it closes."""
+        for sc in self._step_c:
+            sc.update_index = self.updates + 1
+
     def update(self) -> None:
         """Accumulate the last step (call after every VecSwarm.step)."""
+        if self.fused:  # the step did the work
+            self.updates += 1
+            self._next_index()
+            return
         self.vec.join()
         self.updates += 1
         for g in range(self.vec.groups):
@@ -162,6 +174,10 @@ class EvalTracker:
         this after the group's step, for every group once per step, group 0 first."""
         if g == 0:
             self.updates += 1
+        if self.fused:
+            if g == self.vec.groups - 1:
+                self._next_index()
+            return
         nat.check(self.lib.swarm_eval_update(ctypes.byref(self.vec._gparams[g]), ctypes.byref(self._group_c(g)),
                                              ctypes.byref(self.vec._gout[g]), self._stream()), self.lib,
                   which="eval")

@@ -1,5 +1,6 @@
 bash tools/gpu_steps.sh r04c \
  "st256:120:SWARM_STAMPS_KERNEL=n256 SWARM_STAMPS_LIB=build/stamps/libswarm_stamps256.so python tools/stamps.py run 1024 256" \
+ "drvtrace:200:rocprofv3 --kernel-trace -d gpurun_out/r04c/drvtrace -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --cpu-variant-seconds 0" \
  "x3var:300:VAR_BENCH_ARGS='--policy f32x3 --steps 50 --warmup 5' bash tools/run_variants.sh vx3b8 vx3b4late vx3b8" \
  "x3prod:120:python bench.py --policy f32x3 --steps 50 --warmup 5 --no-cpu-baseline --cpu-variant-seconds 0" \
  "evvar:300:VAR_BENCH_ARGS='--groups 2 --eval --steps 500 --warmup 50' bash tools/run_variants.sh vevret vevnofe" \
