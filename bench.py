@@ -116,6 +116,9 @@ def parse(argv=None):
     ap.add_argument("--region-reps", type=int, default=1,
                     help="diagnostic: time the K-step region this many times back to back; the line "
                          "reports the first, `ms_per_step_reps` lists all")
+    ap.add_argument("--events-before", type=int, default=0,
+                    help="eager regions: record the device-time start events before the opening synchronize "
+                         "(1) instead of as the region's first calls (0)")
     ap.add_argument("--spin-sync", action="store_true",
                     help="diagnostic: poll the closing event before the closing synchronize")
     ap.add_argument("--graph-short", action="store_true",
@@ -180,12 +183,16 @@ def max_over_ranks(values, world: int, device=None) -> list[float]:
     return [float(x) for x in t.cpu()]
 
 
-def timed_region(body, world: int, sync, spin=None) -> float:
+def timed_region(body, world: int, sync, spin=None, pre=None) -> float:
     """Barrier + sync, run `body`, sync + barrier; wall seconds of this rank.  `spin`: an event
-    polled until it completes before the closing sync (diagnostic --spin-sync)."""
+    polled until it completes before the closing sync (diagnostic --spin-sync).  `pre`: run
+    before the opening sync (the start events of the device-time bracket: their host cost would
+    otherwise delay the region's first launch)."""
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
+    if pre is not None:
+        pre()
     sync()
     t0 = time.perf_counter()
     body()
@@ -544,13 +551,17 @@ def main(argv=None):
         ev_free = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                    for _ in range(G)] if free else []
 
-        def body():
+        def start_events():
             if free:
                 for (e0, _), st in zip(ev_free, vec.group_streams):
                     e0.record(st)
             else:
                 t_ev[0].record(stream)
                 fork(t_ev[0])
+
+        def body():
+            if not args.events_before:
+                start_events()
             for k in range(args.steps):
                 step(k)
             if free:
@@ -593,14 +604,15 @@ def main(argv=None):
                 sync()
         sync()
         warm_ms = (time.perf_counter() - t0) * 1e3
+    pre = start_events if (not use_graph and args.events_before) else None
     if gatherer is None:
         for _ in range(max(0, args.rehearse)):
-            timed_region(body, world, sync)
+            timed_region(body, world, sync, pre=pre)
     gather_t0 = gatherer.k if gatherer is not None else 0
-    wall = timed_region(body, world, sync, spin=t_ev[1] if args.spin_sync else None)
+    wall = timed_region(body, world, sync, spin=t_ev[1] if args.spin_sync else None, pre=pre)
     walls_rep = [wall]
     for _ in range(args.region_reps - 1):  # diagnostic repeats (not reported as the value)
-        walls_rep.append(timed_region(body, world, sync))
+        walls_rep.append(timed_region(body, world, sync, pre=pre))
     if not use_graph and free:  # first start to last end over the group streams
         f0 = ev_free[0][0]
         kern_ms = (max(f0.elapsed_time(e1) for _, e1 in ev_free) -

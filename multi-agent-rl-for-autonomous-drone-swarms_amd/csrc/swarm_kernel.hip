@@ -69,6 +69,7 @@
 #define ABL_PHILOX 8192     // step64: reset draws from one multiply-xor per word instead of Philox
 #define ABL_EXSEL 16384     // step64: the general finish without exact_select (its answer kept)
 #define ABL_GENKEEP 32768   // step64: the fast finish's checks and ballot kept, the general finish skipped
+#define ABL_ROWGATHER 65536 // step64: the obs row's neighbour / obstacle columns without their LDS gathers (wrong values)
 
 // Diagnostic phase timestamps (tools/stamps.py; never set in the product build)
 #ifdef SWARM_STAMPS
@@ -2121,8 +2122,12 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
         // path length += |last - p| (evaluate_protocol.py's _distance: the sdot-double norm); last =
         // the position this step started from, still in the state (written back below): an agent
         // observed now was observed at the previous step or stands at its episode's start
+#if SWARM_EVAL_OLDPOS_REG  // the loaded inputs kept in registers through the passes
+        const float inc = sqrt_rn(sqsum_1d(c.px - px, c.py - py, c.pz - pz));
+#else
         const float* po = A->S.pos + ea * 3 + t3;
         const float inc = sqrt_rn(sqsum_1d(po[0] - px, po[1] - py, po[2] - pz));
+#endif
         double* tr = A->EV.traveled + ea + t;
         *tr = *tr + (double)inc;
       }
@@ -2359,12 +2364,12 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
 #pragma unroll
   for (int s = 0; s < S64_K; ++s) {
-    const float4 q = ring[wj[s] & (S64_N - 1)];
+    const float4 q = (SWARM_ABLATE & ABL_ROWGATHER) ? make_float4((float)wj[s], 0.f, 0.f, 0.f) : ring[wj[s] & (S64_N - 1)];
     row[9 + 4 * s] = q.x - px; row[10 + 4 * s] = q.y - py; row[11 + 4 * s] = q.z - pz; row[12 + 4 * s] = wd[s];
   }
 #pragma unroll
   for (int s = 0; s < S64_MS; ++s) {
-    const float4 q = obst[oj[s] & (S64_MMAX - 1)];
+    const float4 q = (SWARM_ABLATE & ABL_ROWGATHER) ? make_float4((float)oj[s], 0.f, 0.f, 0.f) : obst[oj[s] & (S64_MMAX - 1)];
     row[21 + 4 * s] = q.x - px; row[22 + 4 * s] = q.y - py; row[23 + 4 * s] = q.z - pz; row[24 + 4 * s] = od[s];
   }
   if (SWARM_ABLATE & ABL_OBS) return;
@@ -2516,6 +2521,9 @@ swarm_step64_once(const S64Args args) {
 // swarm_kernel<0, DYN_PHYS, 4, 5, 2>, bit for bit.
 // The headline step with the evaluation protocol fused in (out.eval, SWARM_EVAL_STEP_FUSED):
 // a separate instantiation, so the plain step's registers and schedule are untouched.
+#ifndef SWARM_EVAL_OLDPOS_REG
+#define SWARM_EVAL_OLDPOS_REG 0
+#endif
 #ifndef SWARM_S64_EVAL_WAVES
 #define SWARM_S64_EVAL_WAVES 8
 #endif
@@ -3976,7 +3984,41 @@ int step64_grid(const swarm_params_t* p, int E) {
   return g < E ? (int)g : E;
 }
 
+int build_kparams_uncached(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* info);
+// Derived launch parameters of the last few params blocks (every step call derives them; an
+// env-group step derives them once per group): a hit is one memcmp of the 240-B params block.
+struct KpMemo {
+  swarm_params_t p;
+  KParams k;
+  swarm_launch_info_t info;
+  bool valid;
+};
+thread_local KpMemo g_kp_memo[4];
+thread_local int g_kp_memo_next = 0;
 int build_kparams(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* info) {
+  if (p) {
+    for (const KpMemo& m : g_kp_memo) {
+      if (m.valid && memcmp(&m.p, p, sizeof(*p)) == 0) {
+        *kp = m.k;
+        if (info) *info = m.info;
+        return SWARM_OK;
+      }
+    }
+  }
+  swarm_launch_info_t li;
+  const int rc = build_kparams_uncached(p, kp, &li);
+  if (rc == SWARM_OK) {
+    KpMemo& m = g_kp_memo[g_kp_memo_next];
+    g_kp_memo_next = (g_kp_memo_next + 1) % 4;
+    m.p = *p;
+    m.k = *kp;
+    m.info = li;
+    m.valid = true;
+    if (info) *info = li;
+  }
+  return rc;
+}
+int build_kparams_uncached(const swarm_params_t* p, KParams* kp, swarm_launch_info_t* info) {
   if (!p) return fail(SWARM_ENULL, "params is NULL");
   if (p->abi_version != SWARM_ABI_VERSION)
     return fail(SWARM_EINVAL, "abi_version %d != library %d", p->abi_version, SWARM_ABI_VERSION);

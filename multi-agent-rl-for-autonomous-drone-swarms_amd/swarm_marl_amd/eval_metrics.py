@@ -117,7 +117,9 @@ class EvalTracker:
         """Point every group's step launch at this tracker's accumulators (out.eval): group g's
         struct holds its row offsets (swarm_step_groups offsets group 0's by itself)."""
         vec = self.vec
-        self._step_c = [self._group_c(g) for g in range(vec.groups)]
+        # copies: _group_c(g) of one group is self._c, whose update index the launches of
+        # begin() / update() rewrite
+        self._step_c = [nat.SwarmEval.from_buffer_copy(self._group_c(g)) for g in range(vec.groups)]
         for g, sc in enumerate(self._step_c):
             sc.flags = nat.EVAL_STEP_FUSED
             vec._gout[g].eval = ctypes.addressof(sc)
