@@ -116,9 +116,11 @@ def parse(argv=None):
     ap.add_argument("--region-reps", type=int, default=1,
                     help="diagnostic: time the K-step region this many times back to back; the line "
                          "reports the first, `ms_per_step_reps` lists all")
-    ap.add_argument("--events-before", type=int, default=0,
+    ap.add_argument("--events-before", type=int, default=1,
                     help="eager regions: record the device-time start events before the opening synchronize "
-                         "(1) instead of as the region's first calls (0)")
+                         "(1) instead of as the region's first calls (0).  The wall clock is unchanged; the "
+                         "device span then also holds the gap from the synchronize to the first launch "
+                         "(r04e, driver command x3 each: 25.39 vs 26.17 us per step)")
     ap.add_argument("--spin-sync", action="store_true",
                     help="diagnostic: poll the closing event before the closing synchronize")
     ap.add_argument("--graph-short", action="store_true",

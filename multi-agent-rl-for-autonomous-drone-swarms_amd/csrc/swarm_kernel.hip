@@ -33,6 +33,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <type_traits>
 
 #include "swarm_mi355x.h"
 
@@ -161,10 +162,20 @@ __device__ __forceinline__ float sqrt_rn(float x) {
   r = (ep > 0.0f) ? rp : r;
   return r;
 }
+#ifndef SWARM_TINY_CMP
+#define SWARM_TINY_CMP 0
+#endif
+#ifndef SWARM_EVAL_ALL
+#define SWARM_EVAL_ALL 0
+#endif
 // sqrt_rn's fast path alone, for branch-free loops: `tiny` records an input below 2^-96 (the
 // caller redoes the loop with sqrt_rn when any lane saw one; the value returned then is unused)
 __device__ __forceinline__ float sqrt_rn_nb(float x, bool& tiny) {
+#if SWARM_TINY_CMP  // 0 < x < 2^-96 as one unsigned compare (x is a sum of squares: never negative)
+  tiny = tiny | (__float_as_uint(x) - 1u < 0x0F7FFFFFu);
+#else
   tiny = tiny | !(x >= 0x1p-96f || x == 0.0f);
+#endif
   float r = __builtin_amdgcn_sqrtf(x);
   const float rm = __uint_as_float(__float_as_uint(r) - 1u), rp = __uint_as_float(__float_as_uint(r) + 1u);
   const float em = __builtin_fmaf(-rm, r, x), ep = __builtin_fmaf(-rp, r, x);
@@ -188,6 +199,23 @@ __device__ __forceinline__ float sqsum_f(float x, float y, float z) { return ((x
 // contract), so it need not reproduce the reference's bits.
 __device__ __forceinline__ float sqsum_rank(float x, float y, float z) {
   return __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x));
+}
+// A float4 gathered from LDS whose .w the caller ignores: the compiler would read the 12 used bytes
+// with ds_read_b96, banked (a/4) mod 32 in 8-lane groups, so two 16-B entries 128 B apart collide
+// (obstacle j and j + 8).  Keeping .w alive makes it one ds_read_b128, banked (a/4) mod 64 in
+// 16-lane groups: the 16-entry obstacle table is one bank row, conflict-free.
+#ifndef SWARM_LDS128
+#define SWARM_LDS128 1
+#endif
+#ifndef SWARM_S64_KEEPNB
+#define SWARM_S64_KEEPNB 0
+#endif
+__device__ __forceinline__ float4 lds_f4(const float4* __restrict__ p) {
+  const float4 q = *p;
+#if SWARM_LDS128
+  asm volatile("" ::"v"(q.w));
+#endif
+  return q;
 }
 // Whole-wave rotate by one lane (DPP wave_ror:1, gfx9): lane i receives lane i-1's value.
 __device__ __forceinline__ float wave_ror1(float x) {
@@ -539,7 +567,7 @@ __device__ __forceinline__ void obstacle_pass(const float4* __restrict__ obst4, 
                                               bool chk, float s_thr, uint32_t keep,
                                               uint32_t (&ok)[MSL > 0 ? MSL : 1], bool& coll) {
   for (int m = 0; m < M; ++m) {
-    const float4 q = obst4[m];
+    const float4 q = lds_f4(obst4 + m);
     const float s = sqsum_f(q.x - px, q.y - py, q.z - pz);  // exact axis-path value
     if constexpr (MSL > 0) kins<MSL>(ok, (__float_as_uint(s) & keep) | (uint32_t)m);
     if constexpr (COLL) coll = coll || (chk && (s <= s_thr));
@@ -1231,7 +1259,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   if (env_ok && new_episode) {
     for (int m = t; m < M; m += L) {
       float* o = S.obstacles + (env * M + m) * 3;
-      const float4 q = obst4[m];
+      const float4 q = lds_f4(obst4 + m);
       o[0] = q.x; o[1] = q.y; o[2] = q.z;
     }
   }
@@ -1261,7 +1289,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         if (s < K) {
           float f0 = 0.f, f1 = 0.f, f2 = 0.f, f3 = 0.f;
           if (wj[s] < N) {
-            const float4 q = ring[wj[s]];
+            const float4 q = lds_f4(ring + wj[s]);
             f0 = q.x - px; f1 = q.y - py; f2 = q.z - pz; f3 = wd[s];
           }
           row[col + 4 * s + 0] = f0; row[col + 4 * s + 1] = f1;
@@ -1280,7 +1308,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
           if (u == s) { m = oj[u]; d = od[u]; }
       }
       if (m < Me) {
-        const float4 q = obst4[m];
+        const float4 q = lds_f4(obst4 + m);
         f0 = q.x - px; f1 = q.y - py; f2 = q.z - pz; f3 = d;
       }
       row[col + 4 * s + 0] = f0; row[col + 4 * s + 1] = f1;
@@ -1578,6 +1606,25 @@ __device__ __forceinline__ void s64_put_obst(float4* __restrict__ obst, float* _
   os[t] = ox; os[S64_MMAX + t] = oy; os[2 * S64_MMAX + t] = oz;
 }
 
+// Drone j's position for lane t.  Lane j of a step64 wave holds drone j's (post-move) position,
+// the float4 ring's entry: SWARM_S64_BPERM reads it across lanes with ds_bpermute (no LDS banks:
+// a random ds_read_b128 gather of 16-lane groups over the 64-entry ring costs ~2 extra cycles per
+// group in bank conflicts), else from the ring.
+#ifndef SWARM_S64_BPERM
+#define SWARM_S64_BPERM 0
+#endif
+__device__ __forceinline__ float4 s64_ring_gather(const float4* __restrict__ ring, int j, float px, float py,
+                                                  float pz) {
+#if SWARM_S64_BPERM
+  const int a = j << 2;
+  return make_float4(__int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(px))),
+                     __int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(py))),
+                     __int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(pz))), 0.f);
+#else
+  return lds_f4(ring + j);
+#endif
+}
+
 // Drone t's entry of both rings (float4 ring for the finish / obs row, SoA pair-pass ring).
 __device__ __forceinline__ void s64_put(float4* __restrict__ ring, float* __restrict__ soa, int t, float px, float py,
                                         float pz, float w) {
@@ -1604,7 +1651,7 @@ __device__ __forceinline__ uint32_t s64_finish_fast(const uint32_t (&nk)[KS], co
                                                     const float4* __restrict__ ring, const float4* __restrict__ obst,
                                                     int t, int M, uint32_t nb_keep, uint32_t ob_keep, bool dkey,
                                                     float px, float py, float pz, float (&wd)[KS], int (&wj)[KS],
-                                                    float (&od)[MSL], int (&oj)[MSL]) {
+                                                    float (&od)[MSL], int (&oj)[MSL], float (&nd)[3 * (KS - 1)]) {
   constexpr int K = KS - 1, MS = MSL - 1;
   const uint32_t nim = ~nb_keep, oim = ~ob_keep;
   bool near_nb = false, near_ob = false;
@@ -1618,16 +1665,18 @@ __device__ __forceinline__ uint32_t s64_finish_fast(const uint32_t (&nk)[KS], co
 #pragma unroll
   for (int s = 0; s < K; ++s) {
     const int j = (t + (int)(nk[s] & nim)) & (S64_N - 1);
-    const float4 q = ring[j];
-    wd[s] = sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
+    const float4 q = s64_ring_gather(ring, j, px, py, pz);
+    const float dx = q.x - px, dy = q.y - py, dz = q.z - pz;
+    wd[s] = sqrt_rn(sqsum_1d(dx, dy, dz));
     wj[s] = j;
+    nd[3 * s] = dx; nd[3 * s + 1] = dy; nd[3 * s + 2] = dz;  // the obs row's neighbour columns
   }
   wd[K] = __builtin_inff();
   wj[K] = 0x7fffffff;
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
     const int j = (int)(ok[s] & oim);
-    const float4 q = obst[j & (S64_MMAX - 1)];
+    const float4 q = lds_f4(obst + (j & (S64_MMAX - 1)));
     od[s] = sqrt_rn(sqsum_f(q.x - px, q.y - py, q.z - pz));
     oj[s] = j;
   }
@@ -1665,7 +1714,7 @@ __device__ __forceinline__ void s64_finish_general(uint32_t flags, const uint32_
   if (__ballot(near_nb) != 0) {
     // N > KS: slot K is always a drone
     const int j = ((ROT ? t : 0) + (int)(nk[K] & nim)) & (NR - 1);
-    const float4 q = ring[j];
+    const float4 q = lds_f4(ring + j);
     const float d = sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
     if (near_nb) {
       wd[K] = d;
@@ -1686,7 +1735,7 @@ __device__ __forceinline__ void s64_finish_general(uint32_t flags, const uint32_
     const uint32_t key = ok[MS];
     const int j = (int)(key & oim);
     const bool valid = key != KEY_EMPTY && j < M;
-    const float4 q = obst[j & (MMAX - 1)];
+    const float4 q = lds_f4(obst + (j & (MMAX - 1)));
     const float d = sqrt_rn(sqsum_f(q.x - px, q.y - py, q.z - pz));
     if (near_ob) {
       od[MS] = valid ? d : __builtin_inff();
@@ -1970,16 +2019,27 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   // ---- exact top-K (finish_keys, rare exact_select)
   float wd[KS], od[MSL];
   int wj[KS], oj[MSL];
+  // the obs row's neighbour columns p_j - p (SWARM_S64_KEEPNB): the finish's own differences, kept
+  // in registers to the row build instead of a second random ring gather (LDS bank conflicts)
+  float nd[3 * S64_K];
+  auto regather_nd = [&]() {
+#pragma unroll
+    for (int s = 0; s < S64_K; ++s) {
+      const float4 q = s64_ring_gather(ring, wj[s] & (S64_N - 1), px, py, pz);
+      nd[3 * s] = q.x - px; nd[3 * s + 1] = q.y - py; nd[3 * s + 2] = q.z - pz;
+    }
+  };
   auto select_topk = [&](bool dkey) {
     if (SWARM_ABLATE & ABL_FINISH) {  // diagnostic: the keys as the answer (wrong distances)
 #pragma unroll
       for (int s = 0; s < KS; ++s) { wd[s] = __uint_as_float(nk[s] & A->P.nb_keep); wj[s] = (int)(nk[s] & 63u) + t; }
 #pragma unroll
       for (int s = 0; s < MSL; ++s) { od[s] = __uint_as_float(ok[s] & A->P.ob_keep); oj[s] = (int)(ok[s] & 15u); }
+      regather_nd();
       return;
     }
     const uint32_t fflags = s64_finish_fast<KS, MSL>(nk, ok, ring, obst, t, M, A->P.nb_keep, A->P.ob_keep, dkey, px, py,
-                                                     pz, wd, wj, od, oj);
+                                                     pz, wd, wj, od, oj, nd);
     const uint64_t fails = __ballot(fflags != 0);
 #ifdef SWARM_DIAG_FINISH  // diagnostic counters (stamps build): waves / lanes through the general finish
     if (t == 0) {
@@ -2006,9 +2066,11 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       }
     }
 #endif
-    if (SWARM_ABLATE & ABL_EXSEL) return;
-    if (slow_nb) exact_select<KS, false>(ring, S64_N, t, S64_K, max_first(wd, S64_K), px, py, pz, wd, wj);
-    if (slow_ob) exact_select<MSL, true>(obst, M, -1, S64_MS, max_first(od, S64_MS), px, py, pz, od, oj);
+    if (!(SWARM_ABLATE & ABL_EXSEL)) {
+      if (slow_nb) exact_select<KS, false>(ring, S64_N, t, S64_K, max_first(wd, S64_K), px, py, pz, wd, wj);
+      if (slow_ob) exact_select<MSL, true>(obst, M, -1, S64_MS, max_first(od, S64_MS), px, py, pz, od, oj);
+    }
+    if (SWARM_S64_KEEPNB) regather_nd();  // the general finish may have re-ranked the neighbours
   };
   STAMP_AT(srec, 4);
 
@@ -2143,7 +2205,9 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
         // one pass: the square roots without sqrt_rn's per-call slow-path branch (a branch per
         // pair splits the loop into blocks the register allocator spills across); a coincident
         // pair (s' < 2^-96) on any lane redoes the pass with sqrt_rn, bit for bit the same terms
-        auto pass = [&](auto sqrt_fn) -> double {
+        // ALL (every drone observed, the common case): no per-pair observed-mask test
+        auto pass = [&](auto sqrt_fn, auto all_c) -> double {
+          constexpr bool ALL = decltype(all_c)::value;
           // opaque ring base per pass: the two passes' reads must not be merged (96 values
           // would then stay live from the first pass into the second)
           const float* s0 = soa + t;
@@ -2151,7 +2215,8 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
           double s_a = 0.0, s_b = 0.0;  // odd / even rotations (eval_update_kernel's two chains)
           auto term = [&](int r) -> double {
             const float d = sqrt_fn(sqsum_1d(px - s0[r], py - s0[S64_SOA + r], pz - s0[2 * S64_SOA + r]));
-            const bool both = all || (cont && ((m_obs >> ((t + r) & (S64_N - 1))) & 1ull));
+            if constexpr (ALL) return fabs((double)d - sp);
+            const bool both = (SWARM_EVAL_ALL == 0 && all) || (cont && ((m_obs >> ((t + r) & (S64_N - 1))) & 1ull));
             return both ? fabs((double)d - sp) : 0.0;
           };
           // a rolled loop of two rotations: unrolled, the scheduler computes every term up front
@@ -2163,12 +2228,22 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
           }
           s_a += term(31);
           const float d32 = sqrt_fn(sqsum_1d(px - s0[32], py - s0[S64_SOA + 32], pz - s0[2 * S64_SOA + 32]));
-          const bool both32 = cont && ((m_obs >> ((t + 32) & (S64_N - 1))) & 1ull);
+          const bool both32 = ALL || (cont && ((m_obs >> ((t + 32) & (S64_N - 1))) & 1ull));
           return 2.0 * (s_a + s_b) + (both32 ? fabs((double)d32 - sp) : 0.0);
         };
         bool tiny = false;
-        double v = pass([&](float x) { return sqrt_rn_nb(x, tiny); });
-        if (__ballot(tiny) != 0) v = pass([](float x) { return sqrt_rn(x); });
+        auto fast = [&](float x) { return sqrt_rn_nb(x, tiny); };
+        auto exact = [](float x) { return sqrt_rn(x); };
+        using F_ = std::false_type;
+#if SWARM_EVAL_ALL
+        using T_ = std::true_type;
+        double v = all ? pass(fast, T_{}) : pass(fast, F_{});
+        if (__ballot(tiny) != 0) v = all ? pass(exact, T_{}) : pass(exact, F_{});
+#else
+        (void)all;
+        double v = pass(fast, F_{});
+        if (__ballot(tiny) != 0) v = pass(exact, F_{});
+#endif
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         fe = s64_uniform(v) / ((double)n_obs * (double)(n_obs - 1));
@@ -2364,12 +2439,18 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
 #pragma unroll
   for (int s = 0; s < S64_K; ++s) {
-    const float4 q = (SWARM_ABLATE & ABL_ROWGATHER) ? make_float4((float)wj[s], 0.f, 0.f, 0.f) : ring[wj[s] & (S64_N - 1)];
-    row[9 + 4 * s] = q.x - px; row[10 + 4 * s] = q.y - py; row[11 + 4 * s] = q.z - pz; row[12 + 4 * s] = wd[s];
+    if (SWARM_S64_KEEPNB) {
+      row[9 + 4 * s] = nd[3 * s]; row[10 + 4 * s] = nd[3 * s + 1]; row[11 + 4 * s] = nd[3 * s + 2];
+    } else {
+      const float4 q = (SWARM_ABLATE & ABL_ROWGATHER) ? make_float4((float)wj[s], 0.f, 0.f, 0.f)
+                                                      : s64_ring_gather(ring, wj[s] & (S64_N - 1), px, py, pz);
+      row[9 + 4 * s] = q.x - px; row[10 + 4 * s] = q.y - py; row[11 + 4 * s] = q.z - pz;
+    }
+    row[12 + 4 * s] = wd[s];
   }
 #pragma unroll
   for (int s = 0; s < S64_MS; ++s) {
-    const float4 q = (SWARM_ABLATE & ABL_ROWGATHER) ? make_float4((float)oj[s], 0.f, 0.f, 0.f) : obst[oj[s] & (S64_MMAX - 1)];
+    const float4 q = (SWARM_ABLATE & ABL_ROWGATHER) ? make_float4((float)oj[s], 0.f, 0.f, 0.f) : lds_f4(obst + (oj[s] & (S64_MMAX - 1)));
     row[21 + 4 * s] = q.x - px; row[22 + 4 * s] = q.y - py; row[23 + 4 * s] = q.z - pz; row[24 + 4 * s] = od[s];
   }
   if (SWARM_ABLATE & ABL_OBS) return;
@@ -3045,12 +3126,12 @@ swarm_step16q(const S64Args args) {
     // this quarter's slots (q = 3 has no neighbour slot: it repeats slot 2, unused)
     const uint32_t kn = q == 0 ? nk[0] : (q == 1 ? nk[1] : nk[2]);
     const int jn = (d + (int)(kn & nim)) & (Q_N - 1);
-    const float4 qn = L.ring[jn];
+    const float4 qn = lds_f4(L.ring + jn);
     ndx = qn.x - px; ndy = qn.y - py; ndz = qn.z - pz;
     nd = sqrt_rn(sqsum_1d(ndx, ndy, ndz));
     const uint32_t ko = q == 0 ? ok[0] : (q == 1 ? ok[1] : (q == 2 ? ok[2] : ok[3]));
     const int jo = (int)(ko & oim) & (Q_MMAX - 1);
-    const float4 qo = L.obst[jo];
+    const float4 qo = lds_f4(L.obst + jo);
     odx = qo.x - px; ody = qo.y - py; odz = qo.z - pz;
     od = sqrt_rn(sqsum_f(odx, ody, odz));
     // survivor bounds (finish_keys' tails) with slot K-1 / Ms-1 from quarters 2 / 3
@@ -3069,14 +3150,14 @@ swarm_step16q(const S64Args args) {
       for (int i = 0; i < 4; ++i) {
         const int r = q + 1 + 4 * i;
         const int j = (d + r) & (Q_N - 1);
-        const float4 pj = L.ring[j];
+        const float4 pj = lds_f4(L.ring + j);
         const float dj = sqrt_rn(sqsum_1d(pj.x - px, pj.y - py, pj.z - pz));
         k4[i] = r < Q_N ? ((q16_key)__float_as_uint(dj) << 32) | (uint32_t)j : ~0ull;
       }
       q16_quad_select4(k4);
       const q16_key k2 = q == 0 ? k4[0] : (q == 1 ? k4[1] : k4[2]);
       nd = __uint_as_float((uint32_t)(k2 >> 32));
-      const float4 qn2 = L.ring[(int)k2 & (Q_N - 1)];
+      const float4 qn2 = lds_f4(L.ring + ((int)k2 & (Q_N - 1)));
       ndx = qn2.x - px; ndy = qn2.y - py; ndz = qn2.z - pz;
       Q16_FLAG(1u);
     }
@@ -3085,14 +3166,14 @@ swarm_step16q(const S64Args args) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = q + 4 * i;
-        const float4 om = L.obst[m];
+        const float4 om = lds_f4(L.obst + m);
         const float dm = sqrt_rn(sqsum_f(om.x - px, om.y - py, om.z - pz));
         k4[i] = m < M ? ((q16_key)__float_as_uint(dm) << 32) | (uint32_t)m : ~0ull;
       }
       q16_quad_select4(k4);
       const q16_key k2 = q == 0 ? k4[0] : (q == 1 ? k4[1] : (q == 2 ? k4[2] : k4[3]));
       od = __uint_as_float((uint32_t)(k2 >> 32));
-      const float4 qo2 = L.obst[(int)k2 & (Q_MMAX - 1)];
+      const float4 qo2 = lds_f4(L.obst + ((int)k2 & (Q_MMAX - 1)));
       odx = qo2.x - px; ody = qo2.y - py; odz = qo2.z - pz;
       Q16_FLAG(16u);
     }
@@ -3499,7 +3580,7 @@ __device__ __forceinline__ uint32_t h_finish_fast(const uint32_t (&nk)[4], const
 #pragma unroll
   for (int s = 0; s < K; ++s) {
     const int j = (int)(nk[s] & nim) & (H_N - 1);
-    const float4 q = ring[j];
+    const float4 q = lds_f4(ring + j);
     wd[s] = sqrt_rn(sqsum_1d(q.x - px, q.y - py, q.z - pz));
     wj[s] = j;
   }
@@ -3508,7 +3589,7 @@ __device__ __forceinline__ uint32_t h_finish_fast(const uint32_t (&nk)[4], const
 #pragma unroll
   for (int s = 0; s < MS; ++s) {
     const int j = (int)(ok[s] & oim);
-    const float4 q = obst[j & (H_MMAX - 1)];
+    const float4 q = lds_f4(obst + (j & (H_MMAX - 1)));
     od[s] = sqrt_rn(sqsum_f(q.x - px, q.y - py, q.z - pz));
     oj[s] = j;
   }
@@ -3786,12 +3867,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
 #pragma unroll
   for (int s = 0; s < H_K; ++s) {
-    const float4 q = L.ring[wj[s] & (H_N - 1)];
+    const float4 q = lds_f4(L.ring + (wj[s] & (H_N - 1)));
     row[9 + 4 * s] = q.x - px; row[10 + 4 * s] = q.y - py; row[11 + 4 * s] = q.z - pz; row[12 + 4 * s] = wd[s];
   }
 #pragma unroll
   for (int s = 0; s < H_MS; ++s) {
-    const float4 q = L.obst[oj[s] & (H_MMAX - 1)];
+    const float4 q = lds_f4(L.obst + (oj[s] & (H_MMAX - 1)));
     row[21 + 4 * s] = q.x - px; row[22 + 4 * s] = q.y - py; row[23 + 4 * s] = q.z - pz; row[24 + 4 * s] = od[s];
   }
   STAMP256(8);

@@ -493,19 +493,44 @@ __device__ __forceinline__ void split8(const f32x16& a, int s, bool act, f16x8& 
 __device__ __forceinline__ f16x8 wlo_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
 }
-// hi*hi into c, the cross terms (scaled by 2^11) into x (hi*lo) and y (lo*hi): three
-// independent accumulator chains, so one wave per SIMD issues the three MFMAs of a k-step back to
-// back without waiting for a dependent result
+// SWARM_POLICY_X3_MERGE (default): hi*hi into c, both cross terms (scaled by 2^11) into x — a
+// dependent 32x32x16 MFMA issues back to back on gfx950 (MI355X_MICROARCH.md: one accumulator
+// chain runs at the full 32 cycles per MFMA), so the second chain costs nothing and the 32
+// registers of a third accumulator pair go to prefetching.  0: hi*lo into x and lo*hi into y.
+#ifndef SWARM_POLICY_X3_MERGE
+#define SWARM_POLICY_X3_MERGE 1
+#endif
+// prefetch (SWARM_POLICY_X3_PF): the next tile's observations during layers 2-3, the next out
+// block's layer-1 lo fragments during the current block's MFMAs, the layer-3 lo fragments at the
+// start of the out block's last W2 batch (one wave per SIMD: nothing else hides a load)
+#ifndef SWARM_POLICY_X3_PF
+#define SWARM_POLICY_X3_PF 0
+#endif
+#define X3_PF_OBS (SWARM_POLICY_X3_PF & 1)
+#define X3_PF_W1 (SWARM_POLICY_X3_PF & 2)
+#define X3_PF_W3 (SWARM_POLICY_X3_PF & 4)
+#define X3_PF_TOUCH (SWARM_POLICY_X3_PF & 8)  // one dword per 128-B line of the next tile's rows (L2 warm-up)
 __device__ __forceinline__ void mfma3(const f16x8& ah, const f16x8& al, const f16x8& bh, const f16x8& bl, f32x16& c,
                                       f32x16& x, f32x16& y) {
   c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
   x = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, x, 0, 0, 0);
+#if SWARM_POLICY_X3_MERGE
+  x = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, x, 0, 0, 0);
+  (void)y;
+#else
   y = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, y, 0, 0, 0);
+#endif
 }
 __device__ __forceinline__ f32x16 x3_sum(const f32x16& c, const f32x16& x, const f32x16& y) {
   f32x16 r;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) r[i] = c[i] + (x[i] + y[i]) * X3_LO_INV;
+  for (int i = 0; i < 16; ++i)
+#if SWARM_POLICY_X3_MERGE
+    r[i] = c[i] + x[i] * X3_LO_INV;
+  (void)y;
+#else
+    r[i] = c[i] + (x[i] + y[i]) * X3_LO_INV;
+#endif
   return r;
 }
 
@@ -541,7 +566,23 @@ policy_mlp_x3(const FwdArgs A) {
   const long long ntiles = (A.rows + 31) / 32;
   const float* b2 = reinterpret_cast<const float*>(lds + L.b2);
   const float* b3 = reinterpret_cast<const float*>(lds + L.b3);
-  for (long long tile = (long long)blockIdx.x * WAVES + wave; tile < ntiles; tile += (long long)gridDim.x * WAVES) {
+  // obs row loads of a tile: x[row][16 ks + 8 h + j] (clamped; the conversion masks k >= in)
+  float xv[KS1 * 8];
+  auto load_obs = [&](long long tile) {
+    const int lane = threadIdx.x & 63, in = IN_C ? IN_C : A.in;
+    const long long row = tile * 32 + (lane & 31);
+    const float* xr = A.obs + (row < A.rows ? row : A.rows - 1) * in;
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 16 * ks + 8 * ((lane >> 5) & 1) + j;
+        xv[ks * 8 + j] = xr[k < in ? k : in - 1];
+      }
+  };
+  const long long tile0 = (long long)blockIdx.x * WAVES + wave;
+  if (X3_PF_OBS && tile0 < ntiles) load_obs(tile0);
+  for (long long tile = tile0; tile < ntiles; tile += (long long)gridDim.x * WAVES) {
     int lane = threadIdx.x & 63, in_r = A.in, out_r = A.out;
     uint32_t sb = 0;
     asm volatile("" : "+v"(lane), "+s"(in_r), "+s"(out_r), "+s"(sb));
@@ -555,18 +596,11 @@ policy_mlp_x3(const FwdArgs A) {
     const f16x8* w3f = reinterpret_cast<const f16x8*>(lds + L.w3);
     const long long row = tile * 32 + n;
     const bool valid = row < A.rows;
+    const long long next_tile = tile + (long long)gridDim.x * WAVES;
     // ---- obs fragments, split: x[row][16 ks + 8 h + j], x[in] = 1 (bias column)
     f16x8 xh[KS1], xl[KS1];
     {
-      const float* xr = A.obs + (valid ? row : A.rows - 1) * in;
-      float xv[KS1 * 8];
-#pragma unroll
-      for (int ks = 0; ks < KS1; ++ks)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = 16 * ks + 8 * h + j;
-          xv[ks * 8 + j] = xr[k < in ? k : in - 1];
-        }
+      if (!X3_PF_OBS) load_obs(tile);
 #pragma unroll
       for (int ks = 0; ks < KS1; ++ks)
 #pragma unroll
@@ -583,12 +617,24 @@ policy_mlp_x3(const FwdArgs A) {
     }
     // ---- layer 1: 256 x (in + 1), relu -> h1 hi / lo (16 k-step fragments each)
     f16x8 h1h[KS2], h1l[KS2];
+    f16x8 w1n[KS1];  // the next out block's lo fragments (X3_PF)
+    if (X3_PF_W1) {
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks) w1n[ks] = wlo_load(WL, lb, sb + (uint32_t)(L.w1 + (size_t)ks * FRAG));
+    }
 #pragma unroll
     for (int ob = 0; ob < OB; ++ob) {
       f32x16 acc = f32x16{}, accx = f32x16{}, accy = f32x16{};
       f16x8 w1l[KS1];
 #pragma unroll
-      for (int ks = 0; ks < KS1; ++ks) w1l[ks] = wlo_load(WL, lb, sb + (uint32_t)(L.w1 + (size_t)(ob * KS1 + ks) * FRAG));
+      for (int ks = 0; ks < KS1; ++ks) {
+        if (X3_PF_W1) w1l[ks] = w1n[ks];
+        else w1l[ks] = wlo_load(WL, lb, sb + (uint32_t)(L.w1 + (size_t)(ob * KS1 + ks) * FRAG));
+      }
+      if (X3_PF_W1 && ob + 1 < OB) {
+#pragma unroll
+        for (int ks = 0; ks < KS1; ++ks) w1n[ks] = wlo_load(WL, lb, sb + (uint32_t)(L.w1 + (size_t)((ob + 1) * KS1 + ks) * FRAG));
+      }
 #pragma unroll
       for (int ks = 0; ks < KS1; ++ks)
         mfma3(w1f[(ob * KS1 + ks) * 64], w1l[ks], xh[ks], xl[ks], acc, accx, accy);
@@ -611,6 +657,14 @@ policy_mlp_x3(const FwdArgs A) {
     f16x8 wlb[2][X3_B];
 #pragma unroll
     for (int u = 0; u < X3_B; ++u) wlb[0][u] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)u * FRAG));
+    // the next tile's observations, in flight through layers 2 and 3
+    if (X3_PF_OBS && next_tile < ntiles) load_obs(next_tile);
+    float touch = 0.f;
+    if (X3_PF_TOUCH && next_tile < ntiles) {
+      const long long first = next_tile * 32 * in, end = (next_tile * 32 + 32 < A.rows ? next_tile * 32 + 32 : A.rows) * in;
+      const long long at = first + 32ll * lane;  // 128 B apart: the 32 rows' 4.7 KB in one instruction
+      touch = A.obs[at < end ? at : end - 1];
+    }
 #pragma unroll
     for (int ob = 0; ob < OB; ++ob) {
       f32x16 acc, accx = f32x16{}, accy = f32x16{};
@@ -634,6 +688,10 @@ policy_mlp_x3(const FwdArgs A) {
           for (int u = 0; u < X3_B; ++u)
             wlb[(bi + 1) & 1][u] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)((bi + 1) * X3_B + u) * FRAG));
         }
+        if (X3_PF_W3 && !X3_EARLY_W3 && kb + X3_B == KS2 && w3lane) {  // layer-3 lo, a batch ahead
+          a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob) * 2 * out * 16));
+          a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob + 1) * 2 * out * 16));
+        }
         f16x8 wh[X3_B];
 #pragma unroll
         for (int u = 0; u < X3_B; ++u) wh[u] = w2f[(ob * KS2 + kb + u) * 64];
@@ -646,7 +704,7 @@ policy_mlp_x3(const FwdArgs A) {
       if (w3lane) {
         a0h = w3f[(2 * ob) * 2 * out + w3idx];
         a1h = w3f[(2 * ob + 1) * 2 * out + w3idx];
-        if (!X3_EARLY_W3) {
+        if (!X3_EARLY_W3 && !X3_PF_W3) {
           a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob) * 2 * out * 16));
           a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob + 1) * 2 * out * 16));
         }
@@ -659,6 +717,7 @@ policy_mlp_x3(const FwdArgs A) {
       __builtin_amdgcn_sched_barrier(0);
     }
     acc3 = x3_sum(acc3, acc3x, acc3y);
+    if (X3_PF_TOUCH) asm volatile("" ::"v"(touch));
     // ---- outputs: lane holds logits m = (i&3) + 8(i>>2) + 4h of its row (out <= 12: i < 8)
     if (A.logits && valid) {
 #pragma unroll
