@@ -208,7 +208,7 @@ __device__ __forceinline__ float sqsum_rank(float x, float y, float z) {
 #define SWARM_LDS128 1
 #endif
 #ifndef SWARM_S64_KEEPNB
-#define SWARM_S64_KEEPNB 0
+#define SWARM_S64_KEEPNB 1
 #endif
 __device__ __forceinline__ float4 lds_f4(const float4* __restrict__ p) {
   const float4 q = *p;

@@ -506,6 +506,18 @@ __device__ __forceinline__ f16x8 wlo_load(__amdgpu_buffer_rsrc_t r, uint32_t vof
 #ifndef SWARM_POLICY_X3_PF
 #define SWARM_POLICY_X3_PF 0
 #endif
+#ifndef SWARM_POLICY_X3_PIPE
+#define SWARM_POLICY_X3_PIPE 0
+#endif
+#ifndef X3_VALU_PER
+#define X3_VALU_PER 6
+#endif
+#ifndef X3_VALU_PER1
+#define X3_VALU_PER1 10
+#endif
+#if SWARM_POLICY_X3_PIPE && !SWARM_POLICY_X3_MERGE
+#error "SWARM_POLICY_X3_PIPE needs SWARM_POLICY_X3_MERGE (the epilogue sums c + x)"
+#endif
 #define X3_PF_OBS (SWARM_POLICY_X3_PF & 1)
 #define X3_PF_W1 (SWARM_POLICY_X3_PF & 2)
 #define X3_PF_W3 (SWARM_POLICY_X3_PF & 4)
@@ -622,6 +634,16 @@ policy_mlp_x3(const FwdArgs A) {
 #pragma unroll
       for (int ks = 0; ks < KS1; ++ks) w1n[ks] = wlo_load(WL, lb, sb + (uint32_t)(L.w1 + (size_t)ks * FRAG));
     }
+#if SWARM_POLICY_X3_PIPE >= 2
+    // layer 1 pipelined the same way: block ob - 1's split (into h1) sits in block ob's MFMA region;
+    // the last block's split moves into layer 2's first batch (which reads h1 k-steps 0..7 only)
+    f32x16 qc, qx;
+    auto epi1 = [&](int obp) {
+      const f32x16 a = x3_sum(qc, qx, qx);
+      split8(a, 0, true, h1h[2 * obp], h1l[2 * obp]);
+      split8(a, 1, true, h1h[2 * obp + 1], h1l[2 * obp + 1]);
+    };
+#endif
 #pragma unroll
     for (int ob = 0; ob < OB; ++ob) {
       f32x16 acc = f32x16{}, accx = f32x16{}, accy = f32x16{};
@@ -638,10 +660,24 @@ policy_mlp_x3(const FwdArgs A) {
 #pragma unroll
       for (int ks = 0; ks < KS1; ++ks)
         mfma3(w1f[(ob * KS1 + ks) * 64], w1l[ks], xh[ks], xl[ks], acc, accx, accy);
+#if SWARM_POLICY_X3_PIPE >= 2
+      if (ob > 0) {
+        epi1(ob - 1);
+#pragma unroll
+        for (int u = 0; u < 3 * KS1; ++u) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, X3_VALU_PER1, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      qc = acc;
+      qx = accx;
+#else
       acc = x3_sum(acc, accx, accy);
       split8(acc, 0, true, h1h[2 * ob], h1l[2 * ob]);
       split8(acc, 1, true, h1h[2 * ob + 1], h1l[2 * ob + 1]);
       __builtin_amdgcn_sched_barrier(0);
+#endif
     }
     // ---- layer 2 (relu) fused with layer 3: each out block's two split fragments feed layer 3's
     // k-steps 2ob, 2ob+1 at once
@@ -665,6 +701,80 @@ policy_mlp_x3(const FwdArgs A) {
       const long long at = first + 32ll * lane;  // 128 B apart: the 32 rows' 4.7 KB in one instruction
       touch = A.obs[at < end ? at : end - 1];
     }
+#if SWARM_POLICY_X3_PIPE
+    // software-pipelined over out blocks: block ob - 1's epilogue (x3 sum, relu split, its two
+    // layer-3 k-steps) is VALU work independent of block ob's first W2 batch, so it is placed in
+    // that batch's scheduling region, interleaved MFMA / VALU by sched_group_barrier: one wave per
+    // SIMD then keeps the matrix pipe busy while it splits (unpipelined, the split of every block
+    // stalled the MFMAs: PMC r04h, 23.8k non-MFMA VALU per wave against 8k MFMAs)
+    f32x16 pc, pxx;            // block ob - 1's accumulators
+    f16x8 p0l = {}, p1l = {};  // block ob - 1's layer-3 lo fragments (requested during its last batch)
+    auto epilogue = [&](int ob_prev) {
+      const f32x16 a = x3_sum(pc, pxx, pxx);
+      f16x8 a0h = {}, a1h = {};
+      if (w3lane) {
+        a0h = w3f[(2 * ob_prev) * 2 * out + w3idx];
+        a1h = w3f[(2 * ob_prev + 1) * 2 * out + w3idx];
+      }
+      f16x8 h2h, h2l;
+      split8(a, 0, true, h2h, h2l);
+      mfma3(a0h, p0l, h2h, h2l, acc3, acc3x, acc3y);
+      split8(a, 1, true, h2h, h2l);
+      mfma3(a1h, p1l, h2h, h2l, acc3, acc3x, acc3y);
+    };
+#pragma unroll
+    for (int ob = 0; ob < OB; ++ob) {
+      f32x16 acc, accx = f32x16{}, accy = f32x16{};
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 b = *reinterpret_cast<const float4*>(b2 + ob * 32 + 8 * g + 4 * h);
+        acc[4 * g + 0] = b.x; acc[4 * g + 1] = b.y; acc[4 * g + 2] = b.z; acc[4 * g + 3] = b.w;
+      }
+      f16x8 a0l = {}, a1l = {};
+#pragma unroll
+      for (int kb = 0; kb < KS2; kb += X3_B) {
+        const int bi = (ob * KS2 + kb) / X3_B;  // batch index
+        if (bi + 1 < NB2) {
+#pragma unroll
+          for (int u = 0; u < X3_B; ++u)
+            wlb[(bi + 1) & 1][u] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)((bi + 1) * X3_B + u) * FRAG));
+        }
+        if (kb + X3_B == KS2 && w3lane) {  // this block's layer-3 lo, used in the next block's first batch
+          a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob) * 2 * out * 16));
+          a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob + 1) * 2 * out * 16));
+        }
+        f16x8 wh[X3_B];
+#pragma unroll
+        for (int u = 0; u < X3_B; ++u) wh[u] = w2f[(ob * KS2 + kb + u) * 64];
+#pragma unroll
+        for (int u = 0; u < X3_B; ++u) mfma3(wh[u], wlb[bi & 1][u], h1h[kb + u], h1l[kb + u], acc, accx, accy);
+#if SWARM_POLICY_X3_PIPE >= 2
+        if (kb == 0 && ob == 0) {
+          epi1(OB - 1);
+#pragma unroll
+          for (int u = 0; u < 3 * X3_B; ++u) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, X3_VALU_PER, 0);
+          }
+        }
+#endif
+        if (kb == 0 && ob > 0) {
+          epilogue(ob - 1);
+#pragma unroll
+          for (int u = 0; u < 3 * X3_B; ++u) {  // 1 MFMA, then up to X3_VALU_PER vector instructions
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, X3_VALU_PER, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      pc = acc;
+      pxx = accx;
+      p0l = a0l;
+      p1l = a1l;
+    }
+    epilogue(OB - 1);
+#else
 #pragma unroll
     for (int ob = 0; ob < OB; ++ob) {
       f32x16 acc, accx = f32x16{}, accy = f32x16{};
@@ -716,6 +826,7 @@ policy_mlp_x3(const FwdArgs A) {
       mfma3(a1h, a1l, h2h, h2l, acc3, acc3x, acc3y);
       __builtin_amdgcn_sched_barrier(0);
     }
+#endif
     acc3 = x3_sum(acc3, acc3x, acc3y);
     if (X3_PF_TOUCH) asm volatile("" ::"v"(touch));
     // ---- outputs: lane holds logits m = (i&3) + 8(i>>2) + 4h of its row (out <= 12: i < 8)
