@@ -168,6 +168,11 @@ __device__ __forceinline__ float sqrt_rn(float x) {
 #ifndef SWARM_EVAL_ALL
 #define SWARM_EVAL_ALL 0
 #endif
+// diagnostic: parts of the fused eval skipped (1 formation error, 2 path length, 4 episode restart
+// writes, 8 the whole block; timing only, wrong metrics)
+#ifndef SWARM_EVAL_ABL
+#define SWARM_EVAL_ABL 0
+#endif
 // sqrt_rn's fast path alone, for branch-free loops: `tiny` records an input below 2^-96 (the
 // caller redoes the loop with sqrt_rn when any lane saw one; the value returned then is unused)
 __device__ __forceinline__ float sqrt_rn_nb(float x, bool& tiny) {
@@ -2168,7 +2173,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   const uint64_t m_term = __ballot(term), m_trunc = __ballot(trunc);
   bool ev_restart = false;  // fused eval: a live episode ended here and the env restarts
   if constexpr (EVAL) __builtin_amdgcn_sched_barrier(0);  // the finish's reads stay below the eval block
-  if (EVAL && DYN == DYN_KIN && A->EV.status != nullptr) {
+  if (EVAL && DYN == DYN_KIN && !(SWARM_EVAL_ABL & 8) && A->EV.status != nullptr) {
     // fused eval (out.eval, SWARM_EVAL_STEP_FUSED): everything swarm_eval_update does for one step
     // (swarm_eval.hip eval_update_kernel: the same arithmetic, the same f64 butterflies), with the
     // positions already in registers / LDS: episode reward += mean reward of the stepped agents,
@@ -2180,7 +2185,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       const bool not_reached = __ballot(cont && !reached) != 0;
       const uint64_t m_obs = __ballot(cont);
       const int n_obs = __popcll(m_obs);
-      if (cont) {
+      if (cont && !(SWARM_EVAL_ABL & 2)) {
         // path length += |last - p| (evaluate_protocol.py's _distance: the sdot-double norm); last =
         // the position this step started from, still in the state (written back below): an agent
         // observed now was observed at the previous step or stands at its episode's start
@@ -2199,7 +2204,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       // sums end uniform and are moved to SGPRs at once (short VGPR live ranges: the kernel runs
       // at 64 VGPRs)
       double fe = 0.0;
-      if (n_obs > 1) {
+      if (n_obs > 1 && !(SWARM_EVAL_ABL & 1)) {
         const double sp = A->EV.spacing;
         const bool all = n_obs == S64_N;
         // one pass: the square roots without sqrt_rn's per-call slow-path branch (a branch per
@@ -2411,7 +2416,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     gs[3 * S64_N + t3] = vx; gs[3 * S64_N + t3 + 1] = vy; gs[3 * S64_N + t3 + 2] = vz;
     if (t == 0) { gs[6 * S64_N + 0] = gx; gs[6 * S64_N + 1] = gy; gs[6 * S64_N + 2] = gz; }
   }
-  if (EVAL && DYN == DYN_KIN && ev_restart) {
+  if (EVAL && DYN == DYN_KIN && ev_restart && !(SWARM_EVAL_ABL & 4)) {
     // fused eval: the next episode opens from its first observation (eval_update_kernel's
     // restart: start = p, goal = p + obs[6:9] = p + (g - p), path length 0)
     float* st0 = A->EV.start + (ea + t) * 3;
