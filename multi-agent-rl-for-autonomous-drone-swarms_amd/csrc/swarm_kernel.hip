@@ -173,6 +173,7 @@ __device__ __forceinline__ float sqrt_rn(float x) {
 #ifndef SWARM_EVAL_ABL
 #define SWARM_EVAL_ABL 0
 #endif
+
 // sqrt_rn's fast path alone, for branch-free loops: `tiny` records an input below 2^-96 (the
 // caller redoes the loop with sqrt_rn when any lane saw one; the value returned then is unused)
 __device__ __forceinline__ float sqrt_rn_nb(float x, bool& tiny) {

@@ -512,6 +512,11 @@ __device__ __forceinline__ f16x8 wlo_load(__amdgpu_buffer_rsrc_t r, uint32_t vof
 #ifndef X3_VALU_PER
 #define X3_VALU_PER 6
 #endif
+// diagnostic ablations of layer 2 (timing only, wrong logits): 1 no W2 lo loads (hi used), 2 no W2
+// hi LDS reads (lo used), 4 no layer-2 MFMAs
+#ifndef X3_ABL
+#define X3_ABL 0
+#endif
 #ifndef X3_VALU_PER1
 #define X3_VALU_PER1 10
 #endif
@@ -793,7 +798,7 @@ policy_mlp_x3(const FwdArgs A) {
 #pragma unroll
       for (int kb = 0; kb < KS2; kb += X3_B) {
         const int bi = (ob * KS2 + kb) / X3_B;  // batch index
-        if (bi + 1 < NB2) {
+        if (bi + 1 < NB2 && !(X3_ABL & 1)) {
 #pragma unroll
           for (int u = 0; u < X3_B; ++u)
             wlb[(bi + 1) & 1][u] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)((bi + 1) * X3_B + u) * FRAG));
@@ -804,9 +809,15 @@ policy_mlp_x3(const FwdArgs A) {
         }
         f16x8 wh[X3_B];
 #pragma unroll
-        for (int u = 0; u < X3_B; ++u) wh[u] = w2f[(ob * KS2 + kb + u) * 64];
+        for (int u = 0; u < X3_B; ++u) wh[u] = (X3_ABL & 2) ? wlb[bi & 1][u] : w2f[(ob * KS2 + kb + u) * 64];
+        if (!(X3_ABL & 4)) {
 #pragma unroll
-        for (int u = 0; u < X3_B; ++u) mfma3(wh[u], wlb[bi & 1][u], h1h[kb + u], h1l[kb + u], acc, accx, accy);
+          for (int u = 0; u < X3_B; ++u)
+            mfma3(wh[u], (X3_ABL & 1) ? wh[u] : wlb[bi & 1][u], h1h[kb + u], h1l[kb + u], acc, accx, accy);
+        } else {
+#pragma unroll
+          for (int u = 0; u < X3_B; ++u) acc[u] += (float)wh[u][0] * (float)wlb[bi & 1][u][1] + (float)h1h[kb + u][2] + (float)h1l[kb + u][3];
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
       acc = x3_sum(acc, accx, accy);
