@@ -173,6 +173,9 @@ __device__ __forceinline__ float sqrt_rn(float x) {
 #ifndef SWARM_EVAL_ABL
 #define SWARM_EVAL_ABL 0
 #endif
+#ifndef SWARM_EVAL_PF
+#define SWARM_EVAL_PF 0
+#endif
 
 // sqrt_rn's fast path alone, for branch-free loops: `tiny` records an input below 2^-96 (the
 // caller redoes the loop with sqrt_rn when any lane saw one; the value returned then is unused)
@@ -739,13 +742,16 @@ __device__ __forceinline__ bool exact_pair_collision(const float4* __restrict__ 
 #ifndef SWARM_WT_STORES
 #define SWARM_WT_STORES 1
 #endif
+#ifndef SWARM_OBS_STORE_AUX
+#define SWARM_OBS_STORE_AUX 16  // cache-policy bits of the obs buffer stores (16 = sc1)
+#endif
 constexpr int BUF_DWORD3 = 0x00020000;  // gfx9 raw buffer descriptor word 3
 __device__ __forceinline__ void store_obs(float* base, uint32_t nbytes, uint32_t byte_off, float4 v) {
   if constexpr (SWARM_WT_STORES) {
     typedef int v4i __attribute__((ext_vector_type(4)));
     const v4i d = {__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w)};
     __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)nbytes, BUF_DWORD3);
-    __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)byte_off, 0, 16 /* sc1 */);
+    __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)byte_off, 0, SWARM_OBS_STORE_AUX);
   } else {
     *reinterpret_cast<float4*>(reinterpret_cast<char*>(base) + byte_off) = v;
   }
@@ -2182,6 +2188,16 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     // exact formation error of the observed drones, and at an episode's end its record
     const uint8_t status = A->EV.status[env];
     if (status & SWARM_EVAL_LIVE) {
+#if SWARM_EVAL_PF  // the env's accumulators requested before the formation pass (latency hidden by it)
+      int pf_steps = 0, pf_rs = 0;
+      double pf_epr = 0.0, pf_fes = 0.0;
+      if (t == 0) {
+        pf_steps = A->EV.ep_steps[env];
+        pf_rs = A->EV.reached_step[env];
+        pf_epr = A->EV.ep_reward[env];
+        pf_fes = A->EV.fe_sum[env];
+      }
+#endif
       const bool coll = __ballot(cont && collided) != 0;
       const bool not_reached = __ballot(cont && !reached) != 0;
       const uint64_t m_obs = __ballot(cont);
@@ -2272,11 +2288,19 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       for (int o = 32; o > 0; o >>= 1) rsum += __shfl_xor(rsum, o);
       rsum = s64_uniform(rsum);
       if (t == 0) {
+#if SWARM_EVAL_PF
+        const int steps = pf_steps + 1;
+        int rs = pf_rs;
+        if (!not_reached && rs < 0) rs = steps;
+        const double ep_reward = pf_epr + (n_active > 0 ? rsum / (double)n_active : 0.0);
+        const double fe_sum = pf_fes + fe;
+#else
         const int steps = A->EV.ep_steps[env] + 1;
         int rs = A->EV.reached_step[env];
         if (!not_reached && rs < 0) rs = steps;
         const double ep_reward = A->EV.ep_reward[env] + (n_active > 0 ? rsum / (double)n_active : 0.0);
         const double fe_sum = A->EV.fe_sum[env] + fe;
+#endif
         if (!ends) {
           A->EV.ep_reward[env] = ep_reward;
           A->EV.fe_sum[env] = fe_sum;
