@@ -474,8 +474,20 @@ constexpr int X3_B = SWARM_POLICY_X3_BATCH;  // W2 k-steps per lo-fragment batch
 // step for 8-step batches with the fragments requested at their use, profiles/r04c_lines.txt)
 constexpr bool X3_EARLY_W3 = SWARM_POLICY_X3_EARLY_W3 != 0;
 
+// diagnostic ablations (timing only, wrong logits): 1 no W2 lo loads (hi used), 2 no W2 hi LDS
+// reads (lo used), 4 no layer-2 MFMAs, 8 no layer-1 MFMAs, 16 no layer-3 MFMAs, 32 splits as plain
+// f16 conversions
+#ifndef X3_ABL
+#define X3_ABL 0
+#endif
 // 8 accumulator values (sub-block s) -> hi / lo f16 fragments, relu'd first when `act`
 __device__ __forceinline__ void split8(const f32x16& a, int s, bool act, f16x8& hi, f16x8& lo) {
+  if (X3_ABL & 32) {  // diagnostic: f16 conversion only (no relu, no lo part)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) hi[q] = (_Float16)a[8 * s + q];
+    lo = hi;
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     float x0 = a[8 * s + 2 * q], x1 = a[8 * s + 2 * q + 1];
@@ -511,11 +523,6 @@ __device__ __forceinline__ f16x8 wlo_load(__amdgpu_buffer_rsrc_t r, uint32_t vof
 #endif
 #ifndef X3_VALU_PER
 #define X3_VALU_PER 6
-#endif
-// diagnostic ablations of layer 2 (timing only, wrong logits): 1 no W2 lo loads (hi used), 2 no W2
-// hi LDS reads (lo used), 4 no layer-2 MFMAs
-#ifndef X3_ABL
-#define X3_ABL 0
 #endif
 #ifndef X3_VALU_PER1
 #define X3_VALU_PER1 10
@@ -664,7 +671,8 @@ policy_mlp_x3(const FwdArgs A) {
       }
 #pragma unroll
       for (int ks = 0; ks < KS1; ++ks)
-        mfma3(w1f[(ob * KS1 + ks) * 64], w1l[ks], xh[ks], xl[ks], acc, accx, accy);
+        if (X3_ABL & 8) acc[ks] += (float)w1f[(ob * KS1 + ks) * 64][0] * (float)w1l[ks][1] + (float)xh[ks][2] + (float)xl[ks][3];
+        else mfma3(w1f[(ob * KS1 + ks) * 64], w1l[ks], xh[ks], xl[ks], acc, accx, accy);
 #if SWARM_POLICY_X3_PIPE >= 2
       if (ob > 0) {
         epi1(ob - 1);
@@ -832,9 +840,11 @@ policy_mlp_x3(const FwdArgs A) {
       }
       f16x8 h2h, h2l;
       split8(acc, 0, true, h2h, h2l);
-      mfma3(a0h, a0l, h2h, h2l, acc3, acc3x, acc3y);
+      if (X3_ABL & 16) acc3[0] += (float)a0h[0] * (float)a0l[1] + (float)h2h[2] + (float)h2l[3];
+      else mfma3(a0h, a0l, h2h, h2l, acc3, acc3x, acc3y);
       split8(acc, 1, true, h2h, h2l);
-      mfma3(a1h, a1l, h2h, h2l, acc3, acc3x, acc3y);
+      if (X3_ABL & 16) acc3[1] += (float)a1h[0] * (float)a1l[1] + (float)h2h[2] + (float)h2l[3];
+      else mfma3(a1h, a1l, h2h, h2l, acc3, acc3x, acc3y);
       __builtin_amdgcn_sched_barrier(0);
     }
 #endif
