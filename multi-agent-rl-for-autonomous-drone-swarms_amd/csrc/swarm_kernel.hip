@@ -33,7 +33,6 @@
 #include <string.h>
 
 #include <atomic>
-#include <type_traits>
 
 #include "swarm_mi355x.h"
 
@@ -162,29 +161,16 @@ __device__ __forceinline__ float sqrt_rn(float x) {
   r = (ep > 0.0f) ? rp : r;
   return r;
 }
-#ifndef SWARM_TINY_CMP
-#define SWARM_TINY_CMP 0
-#endif
-#ifndef SWARM_EVAL_ALL
-#define SWARM_EVAL_ALL 0
-#endif
 // diagnostic: parts of the fused eval skipped (1 formation error, 2 path length, 4 episode restart
 // writes, 8 the whole block; timing only, wrong metrics)
 #ifndef SWARM_EVAL_ABL
 #define SWARM_EVAL_ABL 0
 #endif
-#ifndef SWARM_EVAL_PF
-#define SWARM_EVAL_PF 0
-#endif
 
 // sqrt_rn's fast path alone, for branch-free loops: `tiny` records an input below 2^-96 (the
 // caller redoes the loop with sqrt_rn when any lane saw one; the value returned then is unused)
 __device__ __forceinline__ float sqrt_rn_nb(float x, bool& tiny) {
-#if SWARM_TINY_CMP  // 0 < x < 2^-96 as one unsigned compare (x is a sum of squares: never negative)
-  tiny = tiny | (__float_as_uint(x) - 1u < 0x0F7FFFFFu);
-#else
   tiny = tiny | !(x >= 0x1p-96f || x == 0.0f);
-#endif
   float r = __builtin_amdgcn_sqrtf(x);
   const float rm = __uint_as_float(__float_as_uint(r) - 1u), rp = __uint_as_float(__float_as_uint(r) + 1u);
   const float em = __builtin_fmaf(-rm, r, x), ep = __builtin_fmaf(-rp, r, x);
@@ -1618,23 +1604,10 @@ __device__ __forceinline__ void s64_put_obst(float4* __restrict__ obst, float* _
   os[t] = ox; os[S64_MMAX + t] = oy; os[2 * S64_MMAX + t] = oz;
 }
 
-// Drone j's position for lane t.  Lane j of a step64 wave holds drone j's (post-move) position,
-// the float4 ring's entry: SWARM_S64_BPERM reads it across lanes with ds_bpermute (no LDS banks:
-// a random ds_read_b128 gather of 16-lane groups over the 64-entry ring costs ~2 extra cycles per
-// group in bank conflicts), else from the ring.
-#ifndef SWARM_S64_BPERM
-#define SWARM_S64_BPERM 0
-#endif
-__device__ __forceinline__ float4 s64_ring_gather(const float4* __restrict__ ring, int j, float px, float py,
-                                                  float pz) {
-#if SWARM_S64_BPERM
-  const int a = j << 2;
-  return make_float4(__int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(px))),
-                     __int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(py))),
-                     __int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(pz))), 0.f);
-#else
+// Drone j's position from the float4 ring (one ds_read_b128; reading it across lanes with
+// ds_bpermute instead conflicts as much and costs more LDS issue cycles)
+__device__ __forceinline__ float4 s64_ring_gather(const float4* __restrict__ ring, int j, float, float, float) {
   return lds_f4(ring + j);
-#endif
 }
 
 // Drone t's entry of both rings (float4 ring for the finish / obs row, SoA pair-pass ring).
@@ -2188,16 +2161,6 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     // exact formation error of the observed drones, and at an episode's end its record
     const uint8_t status = A->EV.status[env];
     if (status & SWARM_EVAL_LIVE) {
-#if SWARM_EVAL_PF  // the env's accumulators requested before the formation pass (latency hidden by it)
-      int pf_steps = 0, pf_rs = 0;
-      double pf_epr = 0.0, pf_fes = 0.0;
-      if (t == 0) {
-        pf_steps = A->EV.ep_steps[env];
-        pf_rs = A->EV.reached_step[env];
-        pf_epr = A->EV.ep_reward[env];
-        pf_fes = A->EV.fe_sum[env];
-      }
-#endif
       const bool coll = __ballot(cont && collided) != 0;
       const bool not_reached = __ballot(cont && !reached) != 0;
       const uint64_t m_obs = __ballot(cont);
@@ -2206,12 +2169,8 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
         // path length += |last - p| (evaluate_protocol.py's _distance: the sdot-double norm); last =
         // the position this step started from, still in the state (written back below): an agent
         // observed now was observed at the previous step or stands at its episode's start
-#if SWARM_EVAL_OLDPOS_REG  // the loaded inputs kept in registers through the passes
-        const float inc = sqrt_rn(sqsum_1d(c.px - px, c.py - py, c.pz - pz));
-#else
         const float* po = A->S.pos + ea * 3 + t3;
         const float inc = sqrt_rn(sqsum_1d(po[0] - px, po[1] - py, po[2] - pz));
-#endif
         double* tr = A->EV.traveled + ea + t;
         *tr = *tr + (double)inc;
       }
@@ -2227,9 +2186,9 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
         // one pass: the square roots without sqrt_rn's per-call slow-path branch (a branch per
         // pair splits the loop into blocks the register allocator spills across); a coincident
         // pair (s' < 2^-96) on any lane redoes the pass with sqrt_rn, bit for bit the same terms
-        // ALL (every drone observed, the common case): no per-pair observed-mask test
-        auto pass = [&](auto sqrt_fn, auto all_c) -> double {
-          constexpr bool ALL = decltype(all_c)::value;
+        // (a separate mask-free instance for the all-observed case measured much slower: more
+        // dependency waits)
+        auto pass = [&](auto sqrt_fn) -> double {
           // opaque ring base per pass: the two passes' reads must not be merged (96 values
           // would then stay live from the first pass into the second)
           const float* s0 = soa + t;
@@ -2237,8 +2196,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
           double s_a = 0.0, s_b = 0.0;  // odd / even rotations (eval_update_kernel's two chains)
           auto term = [&](int r) -> double {
             const float d = sqrt_fn(sqsum_1d(px - s0[r], py - s0[S64_SOA + r], pz - s0[2 * S64_SOA + r]));
-            if constexpr (ALL) return fabs((double)d - sp);
-            const bool both = (SWARM_EVAL_ALL == 0 && all) || (cont && ((m_obs >> ((t + r) & (S64_N - 1))) & 1ull));
+            const bool both = all || (cont && ((m_obs >> ((t + r) & (S64_N - 1))) & 1ull));
             return both ? fabs((double)d - sp) : 0.0;
           };
           // a rolled loop of two rotations: unrolled, the scheduler computes every term up front
@@ -2250,22 +2208,12 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
           }
           s_a += term(31);
           const float d32 = sqrt_fn(sqsum_1d(px - s0[32], py - s0[S64_SOA + 32], pz - s0[2 * S64_SOA + 32]));
-          const bool both32 = ALL || (cont && ((m_obs >> ((t + 32) & (S64_N - 1))) & 1ull));
+          const bool both32 = cont && ((m_obs >> ((t + 32) & (S64_N - 1))) & 1ull);
           return 2.0 * (s_a + s_b) + (both32 ? fabs((double)d32 - sp) : 0.0);
         };
         bool tiny = false;
-        auto fast = [&](float x) { return sqrt_rn_nb(x, tiny); };
-        auto exact = [](float x) { return sqrt_rn(x); };
-        using F_ = std::false_type;
-#if SWARM_EVAL_ALL
-        using T_ = std::true_type;
-        double v = all ? pass(fast, T_{}) : pass(fast, F_{});
-        if (__ballot(tiny) != 0) v = all ? pass(exact, T_{}) : pass(exact, F_{});
-#else
-        (void)all;
-        double v = pass(fast, F_{});
-        if (__ballot(tiny) != 0) v = pass(exact, F_{});
-#endif
+        double v = pass([&](float x) { return sqrt_rn_nb(x, tiny); });
+        if (__ballot(tiny) != 0) v = pass([](float x) { return sqrt_rn(x); });
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         fe = s64_uniform(v) / ((double)n_obs * (double)(n_obs - 1));
@@ -2288,19 +2236,11 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       for (int o = 32; o > 0; o >>= 1) rsum += __shfl_xor(rsum, o);
       rsum = s64_uniform(rsum);
       if (t == 0) {
-#if SWARM_EVAL_PF
-        const int steps = pf_steps + 1;
-        int rs = pf_rs;
-        if (!not_reached && rs < 0) rs = steps;
-        const double ep_reward = pf_epr + (n_active > 0 ? rsum / (double)n_active : 0.0);
-        const double fe_sum = pf_fes + fe;
-#else
         const int steps = A->EV.ep_steps[env] + 1;
         int rs = A->EV.reached_step[env];
         if (!not_reached && rs < 0) rs = steps;
         const double ep_reward = A->EV.ep_reward[env] + (n_active > 0 ? rsum / (double)n_active : 0.0);
         const double fe_sum = A->EV.fe_sum[env] + fe;
-#endif
         if (!ends) {
           A->EV.ep_reward[env] = ep_reward;
           A->EV.fe_sum[env] = fe_sum;
@@ -2632,9 +2572,6 @@ swarm_step64_once(const S64Args args) {
 // swarm_kernel<0, DYN_PHYS, 4, 5, 2>, bit for bit.
 // The headline step with the evaluation protocol fused in (out.eval, SWARM_EVAL_STEP_FUSED):
 // a separate instantiation, so the plain step's registers and schedule are untouched.
-#ifndef SWARM_EVAL_OLDPOS_REG
-#define SWARM_EVAL_OLDPOS_REG 0
-#endif
 #ifndef SWARM_S64_EVAL_WAVES
 #define SWARM_S64_EVAL_WAVES 8
 #endif

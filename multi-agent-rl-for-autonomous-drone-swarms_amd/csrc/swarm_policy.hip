@@ -466,13 +466,10 @@ constexpr float X3_LO_SCALE = 2048.f, X3_LO_INV = 1.f / 2048.f;
 #define SWARM_POLICY_X3_BATCH 8
 #endif
 constexpr int X3_B = SWARM_POLICY_X3_BATCH;  // W2 k-steps per lo-fragment batch (divides 16)
-#ifndef SWARM_POLICY_X3_EARLY_W3
-#define SWARM_POLICY_X3_EARLY_W3 0
-#endif
-// layer-3 lo fragments requested at the top of their out block (fits the 512 registers only
-// with 4-k-step W2 batches, and measured slower that way: 322.8 / 328.6 vs 314-315 us per rollout
-// step for 8-step batches with the fragments requested at their use, profiles/r04c_lines.txt)
-constexpr bool X3_EARLY_W3 = SWARM_POLICY_X3_EARLY_W3 != 0;
+// Tried and measured slower or equal: three accumulator chains (hi*lo and
+// lo*hi apart), layer-3 lo fragments requested a block early, W1 / W3 lo fragments a block ahead,
+// the next tile's observations prefetched into registers (spills) or touched into L2, and the
+// out-block epilogues software-pipelined into the next block's MFMAs with sched_group_barrier.
 
 // diagnostic ablations (timing only, wrong logits): 1 no W2 lo loads (hi used), 2 no W2 hi LDS
 // reads (lo used), 4 no layer-2 MFMAs, 8 no layer-1 MFMAs, 16 no layer-3 MFMAs, 32 splits as plain
@@ -505,56 +502,19 @@ __device__ __forceinline__ void split8(const f32x16& a, int s, bool act, f16x8& 
 __device__ __forceinline__ f16x8 wlo_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
 }
-// SWARM_POLICY_X3_MERGE (default): hi*hi into c, both cross terms (scaled by 2^11) into x — a
-// dependent 32x32x16 MFMA issues back to back on gfx950 (MI355X_MICROARCH.md: one accumulator
-// chain runs at the full 32 cycles per MFMA), so the second chain costs nothing and the 32
-// registers of a third accumulator pair go to prefetching.  0: hi*lo into x and lo*hi into y.
-#ifndef SWARM_POLICY_X3_MERGE
-#define SWARM_POLICY_X3_MERGE 1
-#endif
-// prefetch (SWARM_POLICY_X3_PF): the next tile's observations during layers 2-3, the next out
-// block's layer-1 lo fragments during the current block's MFMAs, the layer-3 lo fragments at the
-// start of the out block's last W2 batch (one wave per SIMD: nothing else hides a load)
-#ifndef SWARM_POLICY_X3_PF
-#define SWARM_POLICY_X3_PF 0
-#endif
-#ifndef SWARM_POLICY_X3_PIPE
-#define SWARM_POLICY_X3_PIPE 0
-#endif
-#ifndef X3_VALU_PER
-#define X3_VALU_PER 6
-#endif
-#ifndef X3_VALU_PER1
-#define X3_VALU_PER1 10
-#endif
-#if SWARM_POLICY_X3_PIPE && !SWARM_POLICY_X3_MERGE
-#error "SWARM_POLICY_X3_PIPE needs SWARM_POLICY_X3_MERGE (the epilogue sums c + x)"
-#endif
-#define X3_PF_OBS (SWARM_POLICY_X3_PF & 1)
-#define X3_PF_W1 (SWARM_POLICY_X3_PF & 2)
-#define X3_PF_W3 (SWARM_POLICY_X3_PF & 4)
-#define X3_PF_TOUCH (SWARM_POLICY_X3_PF & 8)  // one dword per 128-B line of the next tile's rows (L2 warm-up)
+// hi*hi into c, both cross terms (scaled by 2^11) into x: a dependent 32x32x16 MFMA issues back to
+// back on gfx950 (MI355X_MICROARCH.md: one accumulator chain runs at the full 32 cycles per MFMA),
+// so a second cross-term chain buys nothing and costs 16 registers per accumulator set
 __device__ __forceinline__ void mfma3(const f16x8& ah, const f16x8& al, const f16x8& bh, const f16x8& bl, f32x16& c,
-                                      f32x16& x, f32x16& y) {
+                                      f32x16& x) {
   c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
   x = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, x, 0, 0, 0);
-#if SWARM_POLICY_X3_MERGE
   x = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, x, 0, 0, 0);
-  (void)y;
-#else
-  y = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, y, 0, 0, 0);
-#endif
 }
-__device__ __forceinline__ f32x16 x3_sum(const f32x16& c, const f32x16& x, const f32x16& y) {
+__device__ __forceinline__ f32x16 x3_sum(const f32x16& c, const f32x16& x) {
   f32x16 r;
 #pragma unroll
-  for (int i = 0; i < 16; ++i)
-#if SWARM_POLICY_X3_MERGE
-    r[i] = c[i] + x[i] * X3_LO_INV;
-  (void)y;
-#else
-    r[i] = c[i] + (x[i] + y[i]) * X3_LO_INV;
-#endif
+  for (int i = 0; i < 16; ++i) r[i] = c[i] + x[i] * X3_LO_INV;
   return r;
 }
 
@@ -590,23 +550,7 @@ policy_mlp_x3(const FwdArgs A) {
   const long long ntiles = (A.rows + 31) / 32;
   const float* b2 = reinterpret_cast<const float*>(lds + L.b2);
   const float* b3 = reinterpret_cast<const float*>(lds + L.b3);
-  // obs row loads of a tile: x[row][16 ks + 8 h + j] (clamped; the conversion masks k >= in)
-  float xv[KS1 * 8];
-  auto load_obs = [&](long long tile) {
-    const int lane = threadIdx.x & 63, in = IN_C ? IN_C : A.in;
-    const long long row = tile * 32 + (lane & 31);
-    const float* xr = A.obs + (row < A.rows ? row : A.rows - 1) * in;
-#pragma unroll
-    for (int ks = 0; ks < KS1; ++ks)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 16 * ks + 8 * ((lane >> 5) & 1) + j;
-        xv[ks * 8 + j] = xr[k < in ? k : in - 1];
-      }
-  };
-  const long long tile0 = (long long)blockIdx.x * WAVES + wave;
-  if (X3_PF_OBS && tile0 < ntiles) load_obs(tile0);
-  for (long long tile = tile0; tile < ntiles; tile += (long long)gridDim.x * WAVES) {
+  for (long long tile = (long long)blockIdx.x * WAVES + wave; tile < ntiles; tile += (long long)gridDim.x * WAVES) {
     int lane = threadIdx.x & 63, in_r = A.in, out_r = A.out;
     uint32_t sb = 0;
     asm volatile("" : "+v"(lane), "+s"(in_r), "+s"(out_r), "+s"(sb));
@@ -620,11 +564,18 @@ policy_mlp_x3(const FwdArgs A) {
     const f16x8* w3f = reinterpret_cast<const f16x8*>(lds + L.w3);
     const long long row = tile * 32 + n;
     const bool valid = row < A.rows;
-    const long long next_tile = tile + (long long)gridDim.x * WAVES;
     // ---- obs fragments, split: x[row][16 ks + 8 h + j], x[in] = 1 (bias column)
     f16x8 xh[KS1], xl[KS1];
     {
-      if (!X3_PF_OBS) load_obs(tile);
+      const float* xr = A.obs + (valid ? row : A.rows - 1) * in;
+      float xv[KS1 * 8];
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 16 * ks + 8 * h + j;
+          xv[ks * 8 + j] = xr[k < in ? k : in - 1];
+        }
 #pragma unroll
       for (int ks = 0; ks < KS1; ++ks)
 #pragma unroll
@@ -641,60 +592,25 @@ policy_mlp_x3(const FwdArgs A) {
     }
     // ---- layer 1: 256 x (in + 1), relu -> h1 hi / lo (16 k-step fragments each)
     f16x8 h1h[KS2], h1l[KS2];
-    f16x8 w1n[KS1];  // the next out block's lo fragments (X3_PF)
-    if (X3_PF_W1) {
-#pragma unroll
-      for (int ks = 0; ks < KS1; ++ks) w1n[ks] = wlo_load(WL, lb, sb + (uint32_t)(L.w1 + (size_t)ks * FRAG));
-    }
-#if SWARM_POLICY_X3_PIPE >= 2
-    // layer 1 pipelined the same way: block ob - 1's split (into h1) sits in block ob's MFMA region;
-    // the last block's split moves into layer 2's first batch (which reads h1 k-steps 0..7 only)
-    f32x16 qc, qx;
-    auto epi1 = [&](int obp) {
-      const f32x16 a = x3_sum(qc, qx, qx);
-      split8(a, 0, true, h1h[2 * obp], h1l[2 * obp]);
-      split8(a, 1, true, h1h[2 * obp + 1], h1l[2 * obp + 1]);
-    };
-#endif
 #pragma unroll
     for (int ob = 0; ob < OB; ++ob) {
-      f32x16 acc = f32x16{}, accx = f32x16{}, accy = f32x16{};
+      f32x16 acc = f32x16{}, accx = f32x16{};
       f16x8 w1l[KS1];
 #pragma unroll
+      for (int ks = 0; ks < KS1; ++ks) w1l[ks] = wlo_load(WL, lb, sb + (uint32_t)(L.w1 + (size_t)(ob * KS1 + ks) * FRAG));
+#pragma unroll
       for (int ks = 0; ks < KS1; ++ks) {
-        if (X3_PF_W1) w1l[ks] = w1n[ks];
-        else w1l[ks] = wlo_load(WL, lb, sb + (uint32_t)(L.w1 + (size_t)(ob * KS1 + ks) * FRAG));
-      }
-      if (X3_PF_W1 && ob + 1 < OB) {
-#pragma unroll
-        for (int ks = 0; ks < KS1; ++ks) w1n[ks] = wlo_load(WL, lb, sb + (uint32_t)(L.w1 + (size_t)((ob + 1) * KS1 + ks) * FRAG));
-      }
-#pragma unroll
-      for (int ks = 0; ks < KS1; ++ks)
         if (X3_ABL & 8) acc[ks] += (float)w1f[(ob * KS1 + ks) * 64][0] * (float)w1l[ks][1] + (float)xh[ks][2] + (float)xl[ks][3];
-        else mfma3(w1f[(ob * KS1 + ks) * 64], w1l[ks], xh[ks], xl[ks], acc, accx, accy);
-#if SWARM_POLICY_X3_PIPE >= 2
-      if (ob > 0) {
-        epi1(ob - 1);
-#pragma unroll
-        for (int u = 0; u < 3 * KS1; ++u) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, X3_VALU_PER1, 0);
-        }
+        else mfma3(w1f[(ob * KS1 + ks) * 64], w1l[ks], xh[ks], xl[ks], acc, accx);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      qc = acc;
-      qx = accx;
-#else
-      acc = x3_sum(acc, accx, accy);
+      acc = x3_sum(acc, accx);
       split8(acc, 0, true, h1h[2 * ob], h1l[2 * ob]);
       split8(acc, 1, true, h1h[2 * ob + 1], h1l[2 * ob + 1]);
       __builtin_amdgcn_sched_barrier(0);
-#endif
     }
     // ---- layer 2 (relu) fused with layer 3: each out block's two split fragments feed layer 3's
     // k-steps 2ob, 2ob+1 at once
-    f32x16 acc3, acc3x = f32x16{}, acc3y = f32x16{};
+    f32x16 acc3, acc3x = f32x16{};
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -706,102 +622,13 @@ policy_mlp_x3(const FwdArgs A) {
     f16x8 wlb[2][X3_B];
 #pragma unroll
     for (int u = 0; u < X3_B; ++u) wlb[0][u] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)u * FRAG));
-    // the next tile's observations, in flight through layers 2 and 3
-    if (X3_PF_OBS && next_tile < ntiles) load_obs(next_tile);
-    float touch = 0.f;
-    if (X3_PF_TOUCH && next_tile < ntiles) {
-      const long long first = next_tile * 32 * in, end = (next_tile * 32 + 32 < A.rows ? next_tile * 32 + 32 : A.rows) * in;
-      const long long at = first + 32ll * lane;  // 128 B apart: the 32 rows' 4.7 KB in one instruction
-      touch = A.obs[at < end ? at : end - 1];
-    }
-#if SWARM_POLICY_X3_PIPE
-    // software-pipelined over out blocks: block ob - 1's epilogue (x3 sum, relu split, its two
-    // layer-3 k-steps) is VALU work independent of block ob's first W2 batch, so it is placed in
-    // that batch's scheduling region, interleaved MFMA / VALU by sched_group_barrier: one wave per
-    // SIMD then keeps the matrix pipe busy while it splits (unpipelined, the split of every block
-    // stalled the MFMAs: PMC r04h, 23.8k non-MFMA VALU per wave against 8k MFMAs)
-    f32x16 pc, pxx;            // block ob - 1's accumulators
-    f16x8 p0l = {}, p1l = {};  // block ob - 1's layer-3 lo fragments (requested during its last batch)
-    auto epilogue = [&](int ob_prev) {
-      const f32x16 a = x3_sum(pc, pxx, pxx);
-      f16x8 a0h = {}, a1h = {};
-      if (w3lane) {
-        a0h = w3f[(2 * ob_prev) * 2 * out + w3idx];
-        a1h = w3f[(2 * ob_prev + 1) * 2 * out + w3idx];
-      }
-      f16x8 h2h, h2l;
-      split8(a, 0, true, h2h, h2l);
-      mfma3(a0h, p0l, h2h, h2l, acc3, acc3x, acc3y);
-      split8(a, 1, true, h2h, h2l);
-      mfma3(a1h, p1l, h2h, h2l, acc3, acc3x, acc3y);
-    };
 #pragma unroll
     for (int ob = 0; ob < OB; ++ob) {
-      f32x16 acc, accx = f32x16{}, accy = f32x16{};
+      f32x16 acc, accx = f32x16{};
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 b = *reinterpret_cast<const float4*>(b2 + ob * 32 + 8 * g + 4 * h);
         acc[4 * g + 0] = b.x; acc[4 * g + 1] = b.y; acc[4 * g + 2] = b.z; acc[4 * g + 3] = b.w;
-      }
-      f16x8 a0l = {}, a1l = {};
-#pragma unroll
-      for (int kb = 0; kb < KS2; kb += X3_B) {
-        const int bi = (ob * KS2 + kb) / X3_B;  // batch index
-        if (bi + 1 < NB2) {
-#pragma unroll
-          for (int u = 0; u < X3_B; ++u)
-            wlb[(bi + 1) & 1][u] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)((bi + 1) * X3_B + u) * FRAG));
-        }
-        if (kb + X3_B == KS2 && w3lane) {  // this block's layer-3 lo, used in the next block's first batch
-          a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob) * 2 * out * 16));
-          a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob + 1) * 2 * out * 16));
-        }
-        f16x8 wh[X3_B];
-#pragma unroll
-        for (int u = 0; u < X3_B; ++u) wh[u] = w2f[(ob * KS2 + kb + u) * 64];
-#pragma unroll
-        for (int u = 0; u < X3_B; ++u) mfma3(wh[u], wlb[bi & 1][u], h1h[kb + u], h1l[kb + u], acc, accx, accy);
-#if SWARM_POLICY_X3_PIPE >= 2
-        if (kb == 0 && ob == 0) {
-          epi1(OB - 1);
-#pragma unroll
-          for (int u = 0; u < 3 * X3_B; ++u) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, X3_VALU_PER, 0);
-          }
-        }
-#endif
-        if (kb == 0 && ob > 0) {
-          epilogue(ob - 1);
-#pragma unroll
-          for (int u = 0; u < 3 * X3_B; ++u) {  // 1 MFMA, then up to X3_VALU_PER vector instructions
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, X3_VALU_PER, 0);
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      pc = acc;
-      pxx = accx;
-      p0l = a0l;
-      p1l = a1l;
-    }
-    epilogue(OB - 1);
-#else
-#pragma unroll
-    for (int ob = 0; ob < OB; ++ob) {
-      f32x16 acc, accx = f32x16{}, accy = f32x16{};
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 b = *reinterpret_cast<const float4*>(b2 + ob * 32 + 8 * g + 4 * h);
-        acc[4 * g + 0] = b.x; acc[4 * g + 1] = b.y; acc[4 * g + 2] = b.z; acc[4 * g + 3] = b.w;
-      }
-      // this block's layer-3 lo fragments (k-steps 2ob, 2ob+1): requested a whole block ahead of use
-      // (one wave per SIMD: nothing else hides the L2 round trip)
-      f16x8 a0l = {}, a1l = {};
-      if (X3_EARLY_W3 && w3lane) {
-        a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob) * 2 * out * 16));
-        a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob + 1) * 2 * out * 16));
       }
 #pragma unroll
       for (int kb = 0; kb < KS2; kb += X3_B) {
@@ -811,45 +638,37 @@ policy_mlp_x3(const FwdArgs A) {
           for (int u = 0; u < X3_B; ++u)
             wlb[(bi + 1) & 1][u] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)((bi + 1) * X3_B + u) * FRAG));
         }
-        if (X3_PF_W3 && !X3_EARLY_W3 && kb + X3_B == KS2 && w3lane) {  // layer-3 lo, a batch ahead
-          a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob) * 2 * out * 16));
-          a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob + 1) * 2 * out * 16));
-        }
         f16x8 wh[X3_B];
 #pragma unroll
         for (int u = 0; u < X3_B; ++u) wh[u] = (X3_ABL & 2) ? wlb[bi & 1][u] : w2f[(ob * KS2 + kb + u) * 64];
         if (!(X3_ABL & 4)) {
 #pragma unroll
           for (int u = 0; u < X3_B; ++u)
-            mfma3(wh[u], (X3_ABL & 1) ? wh[u] : wlb[bi & 1][u], h1h[kb + u], h1l[kb + u], acc, accx, accy);
+            mfma3(wh[u], (X3_ABL & 1) ? wh[u] : wlb[bi & 1][u], h1h[kb + u], h1l[kb + u], acc, accx);
         } else {
 #pragma unroll
           for (int u = 0; u < X3_B; ++u) acc[u] += (float)wh[u][0] * (float)wlb[bi & 1][u][1] + (float)h1h[kb + u][2] + (float)h1l[kb + u][3];
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      acc = x3_sum(acc, accx, accy);
-      f16x8 a0h = {}, a1h = {};
-      if (w3lane) {
+      acc = x3_sum(acc, accx);
+      f16x8 a0h = {}, a1h = {}, a0l = {}, a1l = {};
+      if (w3lane) {  // this block's layer-3 fragments (k-steps 2ob, 2ob+1), the lo halves from L2
         a0h = w3f[(2 * ob) * 2 * out + w3idx];
         a1h = w3f[(2 * ob + 1) * 2 * out + w3idx];
-        if (!X3_EARLY_W3 && !X3_PF_W3) {
-          a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob) * 2 * out * 16));
-          a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob + 1) * 2 * out * 16));
-        }
+        a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob) * 2 * out * 16));
+        a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob + 1) * 2 * out * 16));
       }
       f16x8 h2h, h2l;
       split8(acc, 0, true, h2h, h2l);
       if (X3_ABL & 16) acc3[0] += (float)a0h[0] * (float)a0l[1] + (float)h2h[2] + (float)h2l[3];
-      else mfma3(a0h, a0l, h2h, h2l, acc3, acc3x, acc3y);
+      else mfma3(a0h, a0l, h2h, h2l, acc3, acc3x);
       split8(acc, 1, true, h2h, h2l);
       if (X3_ABL & 16) acc3[1] += (float)a1h[0] * (float)a1l[1] + (float)h2h[2] + (float)h2l[3];
-      else mfma3(a1h, a1l, h2h, h2l, acc3, acc3x, acc3y);
+      else mfma3(a1h, a1l, h2h, h2l, acc3, acc3x);
       __builtin_amdgcn_sched_barrier(0);
     }
-#endif
-    acc3 = x3_sum(acc3, acc3x, acc3y);
-    if (X3_PF_TOUCH) asm volatile("" ::"v"(touch));
+    acc3 = x3_sum(acc3, acc3x);
     // ---- outputs: lane holds logits m = (i&3) + 8(i>>2) + 4h of its row (out <= 12: i < 8)
     if (A.logits && valid) {
 #pragma unroll
