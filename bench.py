@@ -56,7 +56,7 @@ MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3, "f32x3": 2500.0 / 3}
 # BASELINE.json configs, per GPU: [2] is the headline (the metric's config), [1] and [4] have
 # their own bench lines (profiles/r02_config_lines.jsonl).
 PRESETS = {
-    "headline": dict(drones=64, envs=8192, ctde=False, groups=2, groups_graph=4,
+    "headline": dict(drones=64, envs=8192, ctde=False, groups=3, groups_graph=4,
                      label="config 3: N=64 x E=8192 on 1 MI355X (headline); config 4 per GPU"),
     "n16": dict(drones=16, envs=1024, ctde=False,
                 label="config 2: N=16 x E=1024 on 1 MI355X (launch-latency-bound)"),
@@ -104,15 +104,15 @@ def parse(argv=None):
                          "warm-up steps (GPU clocks ramp over ~100 ms; reported in the JSON line)")
     ap.add_argument("--groups", type=int, default=None,
                     help="env groups per GPU, each stepped on its own HIP stream (VecSwarm groups=G); "
-                         "default for the headline and n256: 4 with graph replay (K > 256), else 2; 1 for n16")
+                         "default: 4 with graph replay (K > 256), else the preset's (headline 3, n256 2); 1 for n16")
     ap.add_argument("--graph", choices=("split", "fused"), default="split",
                     help="env groups in the timed hipGraph: one graph per group stream, or one graph "
                          "holding every group's chain (fork/join captured)")
     ap.add_argument("--rehearse", type=int, default=3,
                     help="untimed runs of the whole K-step region (each between device syncs) after the "
                          "device warm-up, so the timed region follows what it would follow in a loop "
-                         "of such regions, not a 200 ms burst (tools/r03be_cmd.sh: the first region after "
-                         "the burst ran 28.5-29.9 us per step, repeats 26.0-28.0)")
+                         "of such regions, not a 200 ms burst (round 3: the first region after the burst ran "
+                         "28.5-29.9 us per step, repeats 26.0-28.0)")
     ap.add_argument("--region-reps", type=int, default=1,
                     help="diagnostic: time the K-step region this many times back to back; the line "
                          "reports the first, `ms_per_step_reps` lists all")
@@ -149,8 +149,9 @@ def parse(argv=None):
     if a.groups is None:
         # 4 groups where the timed region replays graphs (K > 256, no CTDE gather): 25.2 vs
         # 26.7 us (headline), 56.2 vs 61.0 us (n256); eager short regions (the driver's K = 20)
-        # keep 2 — four streams' eager launches cost the host ~20 us per step and measured
-        # 44-52 us (profiles/r03_groups_ab.jsonl)
+        # use the preset's `groups`: headline 3 (one native call launches them; 3 group streams +
+        # the default stream fit GPU_MAX_HW_QUEUES = 4): 24.88 vs 25.18 us for 2 over 8 + 8
+        # alternating runs (profiles/r04s_groups.txt; 4 groups 25.3-25.4, 1 group 29.2-29.3)
         gathering = a.ctde and (int(os.environ.get("WORLD_SIZE", "1")) > 1
                                 or os.environ.get("SWARM_BENCH_FORCE_GATHER") == "1")
         graph_long = a.steps > 256 and not a.no_graph and not gathering and not a.eval
@@ -452,7 +453,7 @@ def main(argv=None):
     # whole batch's K steps.
     t_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     # short timed regions (the driver's K = 20) launch eagerly: a replayed graph's kernels ran
-    # slower there (27.5-28.8 vs 30.8-32.3 us per step by events, tools/r03x_cmd.sh); graphs for
+    # slower there (27.5-28.8 vs 30.8-32.3 us per step by events, round 3); graphs for
     # long regions, where the host's ~5 us per launch would otherwise matter
     # --eval launches eagerly: a captured swarm_eval_update would replay its capture-time update
     # index, so the records' update order and the update count would be wrong
