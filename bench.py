@@ -156,6 +156,10 @@ def parse(argv=None):
                                 or os.environ.get("SWARM_BENCH_FORCE_GATHER") == "1")
         graph_long = a.steps > 256 and not a.no_graph and not gathering and not a.eval
         a.groups = pre.get("groups_graph", pre.get("groups", 1)) if graph_long else pre.get("groups", 1)
+        if not graph_long and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            # a multi-rank process also holds RCCL's stream: 2 group streams + the default stream +
+            # RCCL stay within GPU_MAX_HW_QUEUES = 4 (3 groups would make a fifth, sharing a queue)
+            a.groups = min(a.groups, 2)
     if a.groups < 1:
         ap.error("--groups must be >= 1")
 
