@@ -1430,6 +1430,7 @@ union S64Lds {
 // arithmetic per element is sqsum_rank's (fma(z,z, fma(y,y, x*x)) of the same differences).
 typedef float s64_f2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(3))) float s64_lds_cf;
+typedef __attribute__((address_space(1))) uint8_t s64_gu8;
 // F0: key slots filled before this group (the list starts empty at the pass's first group)
 template <int KS, int PASS, bool FAST, int RT, int NB, bool MIRROR, int F0 = (KS > 0 ? KS : 1)>
 __device__ __forceinline__ void pair_group_s64(s64_lds_cf* __restrict__ s0, uint32_t t4, float px, float py, float pz,
@@ -2191,7 +2192,9 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
         auto pass = [&](auto sqrt_fn) -> double {
           // opaque ring base per pass: the two passes' reads must not be merged (96 values
           // would then stay live from the first pass into the second)
-          const float* s0 = soa + t;
+          // (an LDS-typed pointer: a plain `const float*` made opaque loses the address space and
+          // every read became a flat load)
+          s64_lds_cf* s0 = (s64_lds_cf*)(soa + t);
           asm volatile("" : "+v"(s0));
           double s_a = 0.0, s_b = 0.0;  // odd / even rotations (eval_update_kernel's two chains)
           auto term = [&](int r) -> double {
@@ -2349,17 +2352,19 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     const uint64_t m_act = __ballot(new_act);
     // the three row pointers as uniform SGPR values: a lane-selected kernarg field would become
     // a per-lane load whose wait also drains every store issued before it
-    uint8_t* p_term = A->O.terminated;
-    uint8_t* p_trunc = A->O.truncated;
-    uint8_t* p_act = A->S.active;
+    // global-typed: made opaque, a plain pointer loses its address space and the row store becomes
+    // a flat store, which every later `s_waitcnt lgkmcnt` (the obs stage) would also wait for
+    s64_gu8* p_term = (s64_gu8*)A->O.terminated;
+    s64_gu8* p_trunc = (s64_gu8*)A->O.truncated;
+    s64_gu8* p_act = (s64_gu8*)A->S.active;
     asm volatile("" : "+s"(p_term), "+s"(p_trunc), "+s"(p_act));
     const int grp = t >> 4;
     if (grp < 3) {
       const uint64_t m = grp == 0 ? m_term : (grp == 1 ? m_trunc : m_act);
       const uint32_t nib = (uint32_t)(m >> (4 * (t & 15))) & 0xFu;
       const uint32_t word = (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
-      uint8_t* base = grp == 0 ? p_term : (grp == 1 ? p_trunc : p_act);
-      *reinterpret_cast<uint32_t*>(base + ea + 4 * (t & 15)) = word;
+      s64_gu8* base = grp == 0 ? p_term : (grp == 1 ? p_trunc : p_act);
+      *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(base + ea + 4 * (t & 15)) = word;
     }
   }
   if (t == 0) {
@@ -3158,17 +3163,19 @@ swarm_step16q(const S64Args args) {
   }
   {
     const uint64_t m_act = __ballot(new_act);
-    uint8_t* p_term = A->O.terminated;
-    uint8_t* p_trunc = A->O.truncated;
-    uint8_t* p_act = A->S.active;
+    // global-typed: made opaque, a plain pointer loses its address space and the row store becomes
+    // a flat store, which every later `s_waitcnt lgkmcnt` (the obs stage) would also wait for
+    s64_gu8* p_term = (s64_gu8*)A->O.terminated;
+    s64_gu8* p_trunc = (s64_gu8*)A->O.truncated;
+    s64_gu8* p_act = (s64_gu8*)A->S.active;
     asm volatile("" : "+s"(p_term), "+s"(p_trunc), "+s"(p_act));
     const int grp = lane >> 2;  // lanes 0-3 terminated, 4-7 truncated, 8-11 active: dword lane & 3
     if (grp < 3) {
       const uint64_t m = grp == 0 ? m_term : (grp == 1 ? m_trunc : m_act);
       const uint32_t nib = (uint32_t)(m >> (16 * (lane & 3)));  // drones 4k .. 4k+3 at bits 0, 4, 8, 12
       const uint32_t word = (nib & 1u) | ((nib >> 4) & 1u) << 8 | ((nib >> 8) & 1u) << 16 | ((nib >> 12) & 1u) << 24;
-      uint8_t* base = grp == 0 ? p_term : (grp == 1 ? p_trunc : p_act);
-      *reinterpret_cast<uint32_t*>(base + ea + 4 * (lane & 3)) = word;
+      s64_gu8* base = grp == 0 ? p_term : (grp == 1 ? p_trunc : p_act);
+      *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(base + ea + 4 * (lane & 3)) = word;
     }
   }
   if (lane == 0) {
