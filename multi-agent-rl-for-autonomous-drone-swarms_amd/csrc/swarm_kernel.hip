@@ -166,9 +166,6 @@ __device__ __forceinline__ float sqrt_rn(float x) {
 #ifndef SWARM_EVAL_ABL
 #define SWARM_EVAL_ABL 0
 #endif
-#ifndef SWARM_EVAL_FE_BF
-#define SWARM_EVAL_FE_BF 0
-#endif
 
 // sqrt_rn's fast path alone, for branch-free loops: `tiny` records an input below 2^-96 (the
 // caller redoes the loop with sqrt_rn when any lane saw one; the value returned then is unused)
@@ -2203,15 +2200,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
           auto term = [&](int r) -> double {
             const float d = sqrt_fn(sqsum_1d(px - s0[r], py - s0[S64_SOA + r], pz - s0[2 * S64_SOA + r]));
             const bool both = all || (cont && ((m_obs >> ((t + r) & (S64_N - 1))) & 1ull));
-#if SWARM_EVAL_FE_BF
-            // branch-free mask (the high word's AND also clears the sign: |d - d*|): the two
-            // rotations of an iteration stay one basic block the scheduler can interleave
-            const double v = (double)d - sp;
-            const uint64_t keep = both ? 0x7fffffffffffffffull : 0ull;
-            return __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, v) & keep);
-#else
             return both ? fabs((double)d - sp) : 0.0;
-#endif
           };
           // a rolled loop of two rotations: unrolled, the scheduler computes every term up front
           // and keeps them live for the in-order f64 sums (spills at 64 VGPRs)
