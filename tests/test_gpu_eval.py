@@ -140,7 +140,7 @@ def _run_tracker(dev, fused, groups, native_groups=False, e=64, steps=70):
     return ev.records()
 
 
-@pytest.mark.parametrize("groups,native", [(1, False), (2, False), (2, True)])
+@pytest.mark.parametrize("groups,native", [(1, False), (2, False), (2, True), (3, True)])
 def test_fused_eval_equals_unfused(dev, groups, native):
     """SWARM_EVAL_STEP_FUSED (the step accumulates reward / steps / votes / path length in its
     write-back, swarm_eval_update only the formation error): the same records, bit for bit, as

@@ -99,7 +99,7 @@ def test_groups_validation(dev):
         v.step_group(2, torch.zeros((4, 8, 3), device=dev))
 
 
-@pytest.mark.parametrize("e,n,g,kw", [(8192, 64, 4, {}), (1000, 16, 3, {}), (96, 256, 2, {}),
+@pytest.mark.parametrize("e,n,g,kw", [(8192, 64, 4, {}), (8192, 64, 3, {}), (1000, 16, 3, {}), (96, 256, 2, {}),
                                       (300, 64, 3, {"dynamics": "physics"}), (77, 5, 4, {})])
 def test_step_groups_native_launch(dev, e, n, g, kw):
     """VecSwarm.step_groups (swarm_step_groups: one native call, group g on stream g, no fork or
