@@ -2197,26 +2197,42 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
           s64_lds_cf* s0 = (s64_lds_cf*)(soa + t);
           asm volatile("" : "+v"(s0));
           double s_a = 0.0, s_b = 0.0;  // odd / even rotations (eval_update_kernel's two chains)
-          auto term = [&](int r) -> double {
+          // the term added under the lane's mask (|d - d*| as the add's source modifier: no
+          // select, no zero); adding a skipped 0.0 never changed the sum, so the bits are the same
+          auto add = [&](double& acc, int r) {
             const float d = sqrt_fn(sqsum_1d(px - s0[r], py - s0[S64_SOA + r], pz - s0[2 * S64_SOA + r]));
             const bool both = all || (cont && ((m_obs >> ((t + r) & (S64_N - 1))) & 1ull));
-            return both ? fabs((double)d - sp) : 0.0;
+            if (both) acc += fabs((double)d - sp);
           };
-          // a rolled loop of two rotations: unrolled, the scheduler computes every term up front
-          // and keeps them live for the in-order f64 sums (spills at 64 VGPRs)
 #pragma unroll 1
           for (int r = 1; r < 31; r += 2) {
-            s_a += term(r);
-            s_b += term(r + 1);
+            add(s_a, r);
+            add(s_b, r + 1);
           }
-          s_a += term(31);
-          const float d32 = sqrt_fn(sqsum_1d(px - s0[32], py - s0[S64_SOA + 32], pz - s0[2 * S64_SOA + 32]));
-          const bool both32 = cont && ((m_obs >> ((t + 32) & (S64_N - 1))) & 1ull);
-          return 2.0 * (s_a + s_b) + (both32 ? fabs((double)d32 - sp) : 0.0);
+          add(s_a, 31);
+          double s32 = 0.0;
+          {
+            const float d32 = sqrt_fn(sqsum_1d(px - s0[32], py - s0[S64_SOA + 32], pz - s0[2 * S64_SOA + 32]));
+            const bool both32 = cont && ((m_obs >> ((t + 32) & (S64_N - 1))) & 1ull);
+            if (both32) s32 = fabs((double)d32 - sp);
+          }
+          return 2.0 * (s_a + s_b) + s32;
         };
-        bool tiny = false;
-        double v = pass([&](float x) { return sqrt_rn_nb(x, tiny); });
-        if (__ballot(tiny) != 0) v = pass([](float x) { return sqrt_rn(x); });
+        double v;
+        // no per-pair tiny-input test when the pair pass proves every pair is far from 0: its
+        // nearest distance per lane (the nearest key's truncated d~, or the keyless pass's running
+        // minimum) bounds every exact s from below (d~ >= 2^-47 gives s > 2^-95)
+        const float near = early ? smin : __uint_as_float(nk[0] & A->P.nb_keep);
+        if (fast && __ballot(!(near >= 0x1p-47f)) == 0) {
+          v = pass([](float x) {
+            bool unused = false;
+            return sqrt_rn_nb(x, unused);
+          });
+        } else {
+          bool tiny = false;
+          v = pass([&](float x) { return sqrt_rn_nb(x, tiny); });
+          if (__ballot(tiny) != 0) v = pass([](float x) { return sqrt_rn(x); });
+        }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         fe = s64_uniform(v) / ((double)n_obs * (double)(n_obs - 1));
