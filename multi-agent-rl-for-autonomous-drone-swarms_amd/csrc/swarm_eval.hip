@@ -276,6 +276,27 @@ __global__ void __launch_bounds__(EVAL_THREADS * EVAL_WG_ENVS) eval_update_kerne
     const float d = norm1d_fast(p.x - q.x, p.y - q.y, p.z - q.z);
     const double opp = (p.w != 0.f && q.w != 0.f) ? fabs((double)d - a.spacing) : 0.0;
     fe = wave_sum(2.0 * (s_a + s_b) + opp) / ((double)n_obs * (double)(n_obs - 1));
+  } else if (n_obs > 1 && a.N <= EVAL_THREADS / 2) {
+    // small swarms (config 2: N = 16): P = 64 / next_pow2(N) lanes per drone, lane (i, q) takes
+    // partners j = q, q + P, ... — every ordered pair once, spread over all 64 lanes instead of a
+    // serial N - 1 chain on N lanes; every observed drone divides by the same n - 1, so the mean of
+    // means is the pair sum over n (n - 1) (1e-9 relative: only the f64 summation order differs)
+    int np2 = 1;
+    while (np2 < a.N) np2 <<= 1;
+    const int P = EVAL_THREADS / np2;
+    const int i = t / P, q = t - i * P;
+    double acc = 0.0;
+    if (i < a.N) {
+      const float4 p = pos[i];
+      if (p.w != 0.f) {
+        for (int j = q; j < a.N; j += P) {
+          const float4 o = pos[j];
+          if (j == i || o.w == 0.f) continue;
+          acc += fabs((double)norm1d(p.x - o.x, p.y - o.y, p.z - o.z) - a.spacing);
+        }
+      }
+    }
+    fe = wave_sum(acc) / ((double)n_obs * (double)(n_obs - 1));
   } else if (n_obs > 1) {
     double acc = 0.0;
     for (int i = t; i < a.N; i += EVAL_THREADS) {

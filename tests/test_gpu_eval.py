@@ -72,13 +72,17 @@ def test_eval_replays_reference_episodes(dev, name):
     assert agg["episode_reward_mean"] == pytest.approx(ref["episode_reward_mean"], abs=1e-3)
 
 
-def test_eval_auto_reset_matches_oracle(dev):
+@pytest.mark.parametrize("n", [8, 16, 33])
+def test_eval_auto_reset_matches_oracle(dev, n):
+    """The unfused update kernel (not N = 64) against the oracle's episode metrics with
+    auto-reset: N = 8 / 16 take the small-swarm formation path (several lanes per drone), N = 33
+    the general one."""
     from oracle import eval_oracle as ev_o
     from swarm_marl_amd import VecSwarm
     from swarm_marl_amd import _native as nat
     from swarm_marl_amd.envs.drone_swarm_env import build_step_dicts
     from swarm_marl_amd.eval_metrics import EvalTracker
-    e, n, steps = 96, 8, 60
+    e, steps = (96, 60) if n <= 16 else (32, 40)
     vec = VecSwarm(e, {"num_drones": n, "max_steps": 25}, device=dev, auto_reset=True, seed=5, with_infos=True,
                    with_global_state=True, groups=2)
     vec.reset()
