@@ -72,11 +72,11 @@ def test_eval_replays_reference_episodes(dev, name):
     assert agg["episode_reward_mean"] == pytest.approx(ref["episode_reward_mean"], abs=1e-3)
 
 
-@pytest.mark.parametrize("n", [8, 16, 33])
+@pytest.mark.parametrize("n", [8, 16, 33, 40])
 def test_eval_auto_reset_matches_oracle(dev, n):
     """The unfused update kernel (not N = 64) against the oracle's episode metrics with
-    auto-reset: N = 8 / 16 take the small-swarm formation path (several lanes per drone), N = 33
-    the general one."""
+    auto-reset: N = 8 / 16 take the small-swarm formation path (several lanes per drone), N = 33 /
+    40 the general symmetric-rotation one (odd N, and even N with its opposite pairs)."""
     from oracle import eval_oracle as ev_o
     from swarm_marl_amd import VecSwarm
     from swarm_marl_amd import _native as nat
