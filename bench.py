@@ -4,6 +4,13 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config headline|n16|n256]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
+`--gpus N` alone (no WORLD_SIZE in the environment) makes this process a launcher: it spawns N
+rank processes of this file, one per GPU, before touching the GPU itself, forwards rank 0's JSON
+line and fails if any rank fails.  Under torchrun WORLD_SIZE must equal --gpus.  Fewer visible GPUs
+than ranks is an error (SWARM_BENCH_REHEARSAL=1 shares cuda:0 over gloo; SWARM_BENCH_STANDIN=cpu
+runs the rank plumbing with a CPU stand-in step, for the CPU tests).  The line carries the process
+group's `world_size` and every rank's device (`rank_devices`).
+
 One step = one launch of the fused kernel over the local env shard (integrate, distances,
 collision, formation, rewards, terminations, in-kernel auto-reset, kNN obs) with inputs resident
 in HBM.  Envs are sharded across ranks with no collective on the step path (weak scaling:
@@ -45,10 +52,11 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "agent-steps/sec at N=64 × E=8192 envs, 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU issue peak in instruction-lanes/s: one wave64 VALU instruction per 4 cycles per SIMD
-# (16 lanes/clk) x 1024 SIMDs x 2.4 GHz.  The 157.3 TFLOP/s f32 spec counts a packed FMA as 4
-# FLOPs per lane (MI355X_MICROARCH.md: 64 FLOP/clk/SIMD); SQ_INSTS_VALU x 64 counts instruction-lanes.
-VALU_PEAK_LANE_OPS = 39.3e12
+# VALU issue peak in instruction-lanes/s: a wave64 VALU instruction occupies its SIMD-32 for 2
+# cycles (MI355X_MICROARCH.md "Wave scheduling" and the v_fma_f32 row: 2 cyc throughput; the 4 cycles
+# is what ONE wave alone sustains), so 32 lanes/clk/SIMD x 1024 SIMDs x 2.4 GHz.  SQ_INSTS_VALU x 64
+# counts instruction-lanes.  (Rounds 2-4 priced 4 cycles, 39.3e12, which doubled the VALU fraction.)
+VALU_PEAK_LANE_OPS = 78.6e12
 # dense MFMA peaks, MI355X_MICROARCH.md; f32x3 runs three f16 MFMA passes per f32 product, so the
 # f32-graph FLOPs it can deliver peak at a third of the f16 (= bf16) rate
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3, "f32x3": 2500.0 / 3}
@@ -671,6 +679,15 @@ def main(argv=None):
     wall_max, kern_max, eager_max, kern_eager_max, launch_max, pol_max = max_over_ranks(
         [wall, kern_ms, wall_eager, kern_eager, kern_launch, pol_ms], world, dev)
     done_frac = float((vec.env_done != 0).float().mean())
+    props = torch.cuda.get_device_properties(dev)
+    devs = rank_devices(world, {"rank": rank, "local_rank": local, "device": int(dev.index),
+                                "name": props.name, "pci_bus_id": getattr(props, "pci_bus_id", None),
+                                "uuid": str(getattr(props, "uuid", "")) or None, "env_offset": offset})
+    world_pg = dist.get_world_size() if (world > 1 and dist.is_initialized()) else 1
+    if world_pg != world:
+        raise RuntimeError(f"process group holds {world_pg} ranks, WORLD_SIZE {world}")
+    if world > 1 and not rehearsal and len({(d["device"], d["pci_bus_id"], d["uuid"]) for d in devs}) < world:
+        raise RuntimeError(f"ranks share a GPU (one rank per GPU expected): {devs}")
 
     if rank == 0:
         total = world * e * n * args.steps
@@ -713,7 +730,8 @@ def main(argv=None):
                             "peak": VALU_PEAK_LANE_OPS,
                             "frac": lane_ops / (kern_max * 1e-3) / VALU_PEAK_LANE_OPS,
                             "source": "SQ_INSTS_VALU x 64 lanes from profiles/pmc_traffic.json; peak = "
-                                      "16 lanes/clk/SIMD x 1024 SIMDs x 2.4 GHz"}
+                                      "32 lanes/clk/SIMD (a wave64 instruction holds its SIMD-32 for 2 cycles) "
+                                      "x 1024 SIMDs x 2.4 GHz"}
         metric = METRIC if pol is None else \
             "rollout agent-steps/sec (on-device policy + env step) at N=64 x E=8192 per MI355X"
         if tracker is not None:
@@ -722,6 +740,7 @@ def main(argv=None):
             metric = metric.split(" at N=")[0] + f" at N={n} x E={e} envs per MI355X (not the headline shape)"
         rec = {
             "metric": metric, "value": value, "unit": "agent-steps/s", "n_gpus": world,
+            "world_size": world_pg, "rank_devices": devs,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall_max / args.steps * 1e3,
             **({"ms_per_step_reps": [round(w / args.steps * 1e3, 6) for w in walls_rep]}
                if args.region_reps > 1 else {}),
@@ -780,5 +799,147 @@ def main(argv=None):
         dist.destroy_process_group()
 
 
+# ----------------------------------------------------------------------------- rank launcher
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        return s_.getsockname()[1]
+
+
+def check_world(gpus: int, env=None, device_count=None) -> tuple[int, str | None]:
+    """(world, mode) for this process: mode "launch" = the parent spawns `gpus` ranks (WORLD_SIZE
+    unset, --gpus > 1), None = run as this rank.  Raises SystemExit when the request cannot be met:
+    WORLD_SIZE set and != --gpus, or fewer visible GPUs than ranks (one GPU per rank; the gloo
+    rehearsal SWARM_BENCH_REHEARSAL=1 and the CPU stand-in SWARM_BENCH_STANDIN=cpu put every rank
+    on one device / on the CPU and skip the device check)."""
+    env = os.environ if env is None else env
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    shared = env.get("SWARM_BENCH_REHEARSAL") == "1" or env.get("SWARM_BENCH_STANDIN") == "cpu"
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {gpus}: launch exactly --gpus ranks")
+        mode = None
+    else:
+        world, mode = gpus, ("launch" if gpus > 1 else None)
+    if not shared:
+        if device_count is None:
+            import torch  # counting devices does not initialise the GPU on this image
+            device_count = torch.cuda.device_count()
+        if device_count < world:
+            raise SystemExit(f"bench.py: --gpus {gpus} needs {world} GPUs (one rank per GPU), "
+                             f"{device_count} visible")
+    return world, mode
+
+
+def launch_ranks(gpus: int, argv) -> int:
+    """Parent of a multi-GPU run started as plain `python bench.py --gpus N`: spawn N fresh child
+    processes (this file, same arguments) with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set — before
+    any GPU call here and without re-executing this process — forward rank 0's output, and return
+    non-zero if any rank fails (the others are then stopped)."""
+    import threading
+    port = _free_port()
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(gpus),
+                LOCAL_WORLD_SIZE=str(gpus), GROUP_RANK="0", ROLE_RANK="0")
+    cmd = [sys.executable, "-u", str(Path(__file__).resolve()), *argv]
+    procs = []
+    for r in range(gpus):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r), ROLE_WORLD_SIZE=str(gpus))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    lines: list[str] = []
+
+    def forward():  # rank 0's stdout, line by line, as it arrives
+        for raw in procs[0].stdout:
+            s = raw.decode(errors="replace")
+            lines.append(s)
+            sys.stdout.write(s)
+            sys.stdout.flush()
+    th = threading.Thread(target=forward, daemon=True)
+    th.start()
+    rc = 0
+    live = set(range(gpus))
+    while live:
+        for r in sorted(live):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            live.discard(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                sys.stderr.write(f"bench.py: rank {r} exited with {code}; stopping the other ranks\n")
+                for q in live:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    th.join(timeout=10)
+    if rc == 0:
+        rec = [json.loads(s) for s in lines if s.startswith("{")]
+        if not rec or rec[-1].get("n_gpus") != gpus:
+            sys.stderr.write(f"bench.py: rank 0 reported no JSON line for {gpus} ranks\n")
+            return 1
+    return rc
+
+
+def entry(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    world, mode = check_world(args.gpus)
+    if mode == "launch":
+        return launch_ranks(args.gpus, argv)
+    if os.environ.get("SWARM_BENCH_STANDIN") == "cpu":
+        standin_main(args)
+        return 0
+    main(argv)
+    return 0
+
+
+def standin_main(args) -> None:
+    """SWARM_BENCH_STANDIN=cpu: the rank plumbing of main() (env-var ranks, gloo process group,
+    shard plan, barrier-bracketed timed region, max over ranks, world size and per-rank devices in
+    rank 0's line) with a CPU stand-in for the step, so tests can drive `python bench.py --gpus 2`
+    without a GPU.  Not a measurement: `value` is the stand-in's rate and the line says so."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    offset, e = shard_plan(world, rank, args.envs)
+    x = torch.zeros((e, args.drones, 3))
+
+    def body():
+        for _ in range(args.steps):
+            x.add_(1.0)
+    for _ in range(args.warmup):
+        x.add_(1.0)
+    wall = timed_region(body, world, lambda: None)
+    (wall_max,) = max_over_ranks([wall], world)
+    devs = rank_devices(world, {"rank": rank, "device": "cpu", "env_offset": offset})
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": world * e * args.drones * args.steps / wall_max,
+                          "unit": "agent-steps/s", "n_gpus": world, "world_size": world,
+                          "rank_devices": devs, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": wall_max / args.steps * 1e3, "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                          "standin": "CPU stand-in step (SWARM_BENCH_STANDIN=cpu): rank plumbing only, "
+                                     "not a measurement",
+                          "config": {"workload": f"N={args.drones} drones x E={e} envs per rank (stand-in)",
+                                     "global_envs": world * e, "parallelism": f"env-sharded x{world}"}}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def rank_devices(world: int, mine: dict) -> list[dict]:
+    """Every rank's device record (rank order), gathered outside the timed region."""
+    if world == 1:
+        return [mine]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, mine)
+    return out
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(entry())

@@ -4159,8 +4159,13 @@ int build_kparams_uncached(const swarm_params_t* p, KParams* kp, swarm_launch_in
   {
     const long long blocks = ((long long)k.E + G - 1) / G;
     k.obs_direct = (lanes != 64 && blocks <= 2048) ? 1 : 0;
-    const char* ov = getenv("SWARM_OBS_DIRECT");
-    if (ov && (ov[0] == '0' || ov[0] == '1')) k.obs_direct = ov[0] == '1';
+    // read once per process: the derived parameters are memoised by the params bytes (KpMemo),
+    // so an override set after the first launch would be ignored silently for a cached block
+    static const int obs_direct_override = []() {
+      const char* ov = getenv("SWARM_OBS_DIRECT");
+      return (ov && (ov[0] == '0' || ov[0] == '1')) ? ov[0] - '0' : -1;
+    }();
+    if (obs_direct_override >= 0) k.obs_direct = obs_direct_override;
   }
   // neighbour keys carry the drone index (block) or the rotation offset in [1, L) (wave)
   const int nb_bits = k.log2_lanes;
@@ -4234,7 +4239,9 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   kp.pack_bytes = (kp.N == 64 && mode == MODE_STEP && ((uintptr_t)o->terminated | (uintptr_t)o->truncated |
                                                        (uintptr_t)s->active) % 4 == 0) ? 1 : 0;
   S64Eval ev{};
-  if (o->eval) {
+  // out.eval is a step-only input: reset / observe never touch the eval accumulators (a VecSwarm
+  // passes the same out struct to every mode), so it is neither validated nor used there
+  if (o->eval && mode == MODE_STEP) {
     // fused eval accumulation: the kinematic one-wave-per-env step64 launch only
     const swarm_eval_t* e = o->eval;
     const bool once = mode == MODE_STEP && step64_applies(p, kp) && kp.obs_vec4 && kp.pack_bytes && !s->env_cfg &&

@@ -117,6 +117,11 @@ class EvalTracker:
         """Point every group's step launch at this tracker's accumulators (out.eval): group g's
         struct holds its row offsets (swarm_step_groups offsets group 0's by itself)."""
         vec = self.vec
+        prev = getattr(vec, "_eval_owner", None)
+        if prev is not None and prev is not self and prev.fused:
+            # one fused tracker per VecSwarm: the previous owner goes back to unfused updates
+            # (its update() launches swarm_eval_update again), so neither loses records
+            prev.detach()
         # copies: _group_c(g) of one group is self._c, whose update index the launches of
         # begin() / update() rewrite
         self._step_c = [nat.SwarmEval.from_buffer_copy(self._group_c(g)) for g in range(vec.groups)]
@@ -131,9 +136,11 @@ class EvalTracker:
         accumulates every per-step term itself again."""
         if not self.fused:
             return
-        for g in range(self.vec.groups):
-            self.vec._gout[g].eval = None
         if getattr(self.vec, "_eval_owner", None) is self:
+            # the group structs point at this tracker only while it owns them (a newer fused
+            # tracker has re-pointed them: leave those alone)
+            for g in range(self.vec.groups):
+                self.vec._gout[g].eval = None
             self.vec._eval_owner = None
         self.vec.join()
         self.fused = False

@@ -516,6 +516,11 @@ class VecSwarm:
                              "uniform)")
         e = self.num_envs
         self.join()
+        owner = getattr(self, "_eval_owner", None)
+        if owner is not None and owner.fused:
+            # per-env records move the step to the generic kernel, which has no fused eval: the
+            # tracker goes back to unfused updates (its update() launches swarm_eval_update)
+            owner.detach()
         rebind = False
         if self.env_cfg is None:
             self.env_cfg = torch.zeros((e, nat.ENV_CFG_BYTES), dtype=torch.uint8, device=self.device)

@@ -120,3 +120,59 @@ def test_bench_args_presets():
     assert (a.drones, a.envs, a.ctde) == (256, 1024, True)
     a = bench.parse(["--config", "n256", "--envs", "64"])
     assert a.envs == 64
+
+
+def _run_bench(args, env_extra, timeout=240):
+    import subprocess
+    import sys
+    from pathlib import Path
+    ROOT = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], env=env, cwd=str(ROOT),
+                          capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.timeout(300)
+def test_plain_bench_gpus2_spawns_two_ranks():
+    """`python bench.py --gpus 2` (no torchrun) launches 2 ranks itself (CPU stand-in step)."""
+    import json
+    p = _run_bench(["--gpus", "2", "--steps", "3", "--warmup", "1", "--envs", "16"],
+                   {"SWARM_BENCH_STANDIN": "cpu"})
+    assert p.returncode == 0, p.stderr[-2000:]
+    rec = [json.loads(s) for s in p.stdout.splitlines() if s.startswith("{")]
+    assert len(rec) == 1, p.stdout
+    r = rec[0]
+    assert r["n_gpus"] == 2 and r["world_size"] == 2
+    assert [d["rank"] for d in r["rank_devices"]] == [0, 1]
+    assert [d["env_offset"] for d in r["rank_devices"]] == [0, 16]
+    assert r["config"]["global_envs"] == 32
+
+
+@pytest.mark.timeout(120)
+def test_bench_gpus_more_than_visible_fails():
+    """--gpus 8 with fewer visible GPUs (none here) fails loudly before any rank starts."""
+    p = _run_bench(["--gpus", "8", "--steps", "2"], {})
+    assert p.returncode != 0
+    assert "needs 8 GPUs" in p.stderr
+
+
+def test_check_world_rules():
+    import bench
+    assert bench.check_world(1, env={}, device_count=1) == (1, None)
+    assert bench.check_world(4, env={}, device_count=8) == (4, "launch")
+    assert bench.check_world(2, env={"WORLD_SIZE": "2"}, device_count=2) == (2, None)
+    with pytest.raises(SystemExit, match="WORLD_SIZE=2 but --gpus 4"):
+        bench.check_world(4, env={"WORLD_SIZE": "2"}, device_count=8)
+    with pytest.raises(SystemExit, match="needs 8 GPUs"):
+        bench.check_world(8, env={}, device_count=1)
+    # the one-GPU rehearsal shares cuda:0
+    assert bench.check_world(2, env={"SWARM_BENCH_REHEARSAL": "1"}, device_count=1) == (2, "launch")
+
+
+@pytest.mark.timeout(300)
+def test_launcher_fails_when_a_rank_fails():
+    """A rank that fails makes the launcher exit non-zero (rank 1 gets a bad env count)."""
+    p = _run_bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--envs", "-1"],
+                   {"SWARM_BENCH_STANDIN": "cpu"})
+    assert p.returncode != 0

@@ -155,6 +155,73 @@ def test_fused_eval_equals_unfused(dev, groups, native):
     assert np.array_equal(a, b, equal_nan=True)
 
 
+def _tracker_session(dev, fused, *, reset_observe=False, env_cfg=False, e=64, steps=40):
+    """Steps with a tracker, then (optionally) vec.reset() + vec.observe() + begin() or a per-env
+    config that moves the step off step64, then more steps: the records."""
+    from swarm_marl_amd import VecSwarm
+    from swarm_marl_amd.eval_metrics import EvalTracker
+    vec = VecSwarm(e, {"num_drones": 64, "max_steps": 25}, device=dev, auto_reset=True, seed=5, with_infos=True,
+                   groups=2)
+    vec.reset()
+    ev = EvalTracker(vec, capacity=8192, fused=fused)
+    ev.begin()
+    g = torch.Generator(device=dev).manual_seed(29)
+    for k in range(2 * steps):
+        if k == steps and reset_observe:
+            vec.reset()
+            vec.observe()
+            ev.begin()
+        if k == steps and env_cfg:
+            vec.set_env_config(world_size=20.0)  # the batch value: same results as no record
+            assert not ev.fused
+        vec.step(torch.rand((e, 64, 3), device=dev, generator=g) * 2 - 1)
+        ev.update()
+    return ev.records()
+
+
+def test_fused_tracker_then_reset_observe(dev):
+    """a fused tracker attached, then vec.reset(), vec.observe() and begin()
+    (the out struct with out.eval goes to the reset / observe launches too), then more steps — the
+    same records as an unfused tracker over the same calls."""
+    a = _tracker_session(dev, True, reset_observe=True)
+    b = _tracker_session(dev, False, reset_observe=True)
+    assert len(a) > 64 and np.array_equal(a, b, equal_nan=True)
+
+
+def test_set_env_config_detaches_fused_tracker(dev):
+    """per-env records move the step to the generic kernel; the fused tracker goes
+    back to unfused updates instead of every later step failing."""
+    a = _tracker_session(dev, True, env_cfg=True)
+    b = _tracker_session(dev, False, env_cfg=True)
+    assert len(a) > 64 and np.array_equal(a, b, equal_nan=True)
+
+
+def test_second_fused_tracker_takes_over(dev):
+    """a second fused tracker takes the steps over and the first goes back to
+    unfused updates (both keep recording); the first one's detach() does not unhook the second."""
+    from swarm_marl_amd import VecSwarm
+    from swarm_marl_amd.eval_metrics import EvalTracker
+    e = 64
+    vec = VecSwarm(e, {"num_drones": 64, "max_steps": 25}, device=dev, auto_reset=True, seed=5, with_infos=True)
+    vec.reset()
+    ev1 = EvalTracker(vec, capacity=8192)
+    assert ev1.fused
+    ev2 = EvalTracker(vec, capacity=8192)
+    assert ev2.fused and not ev1.fused and vec._eval_owner is ev2
+    ev1.begin()
+    ev2.begin()
+    g = torch.Generator(device=dev).manual_seed(31)
+    for k in range(60):
+        if k == 20:
+            ev1.detach()  # not the owner: a no-op for the steps
+            assert ev2.fused and vec._gout[0].eval is not None
+        vec.step(torch.rand((e, 64, 3), device=dev, generator=g) * 2 - 1)
+        ev1.update()
+        ev2.update()
+    a, b = ev1.records(), ev2.records()
+    assert len(a) > 32 and np.array_equal(a, b, equal_nan=True)
+
+
 def test_record_blocks_only_for_live_segments(dev):
     """E < 64 envs write min(E, 64) record segments: only those blocks are allocated (ADVICE r03:
     E = 1 at the default capacity took 64 blocks, ~302 MB), also at an env_offset that wraps

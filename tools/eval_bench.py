@@ -18,7 +18,7 @@ K = int(sys.argv[3]) if len(sys.argv) > 3 else 200
 dev = torch.device("cuda", 0)
 vec = VecSwarm(E, {"num_drones": N}, device=dev, auto_reset=True, seed=0, with_infos=True)
 vec.reset()
-ev = EvalTracker(vec, capacity=1 << 21)
+ev = EvalTracker(vec, capacity=1 << 21, fused=False)  # the unfused update kernel, as documented
 ev.begin()
 g = torch.Generator(device=dev).manual_seed(1)
 ring = [torch.rand((E, N, 3), device=dev, generator=g) * 2 - 1 for _ in range(8)]
