@@ -1969,6 +1969,17 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     if (z0 + z1 + z2 + z3 == 1234.5f) fsum += 1.0;
   }
 #endif
+#if SWARM_DIAG_EXTRA_INT
+  {  // diagnostic: SWARM_DIAG_EXTRA_INT dependent-free v_min_u32 / v_max_u32 per wave (the key-insert class)
+    uint32_t z0 = __float_as_uint(px), z1 = __float_as_uint(py), z2 = __float_as_uint(pz), z3 = (uint32_t)t;
+#pragma unroll
+    for (int i = 0; i < SWARM_DIAG_EXTRA_INT / 4; ++i) {
+      z0 = min(z0, z1); z1 = max(z1, z2); z2 = min(z2, z3); z3 = max(z3, z0);
+      asm volatile("" : "+v"(z0), "+v"(z1), "+v"(z2), "+v"(z3));
+    }
+    if (z0 + z1 + z2 + z3 == 12345u) fsum += 1.0;
+  }
+#endif
   if constexpr (DYN == DYN_PHYS) {  // s' keys, no formation; every drone is a contact candidate
     pair_pass_s64<KS, 2, true>(soa, t, px, py, pz, true, A->P.nb_keep, 0.f, nk, smin, fsum);
     obstacle_pass_s64<MSL, true>(osoa, M, px, py, pz, true, A->P.s_phys_obst, A->P.ob_keep, ok, ocoll);
@@ -3685,6 +3696,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   // ---- formation + minimum pass (every pair once), obstacle pass
   double fsum = 0.0;
   float smin = __builtin_inff();
+#if SWARM_DIAG_EXTRA_INT
+  {  // diagnostic: SWARM_DIAG_EXTRA_INT dependent-free v_min_u32 / v_max_u32 per wave
+    uint32_t z0 = __float_as_uint(px), z1 = __float_as_uint(py), z2 = __float_as_uint(pz), z3 = (uint32_t)t;
+#pragma unroll
+    for (int q = 0; q < SWARM_DIAG_EXTRA_INT / 4; ++q) {
+      z0 = min(z0, z1); z1 = max(z1, z2); z2 = min(z2, z3); z3 = max(z3, z0);
+      asm volatile("" : "+v"(z0), "+v"(z1), "+v"(z2), "+v"(z3));
+    }
+    if (z0 + z1 + z2 + z3 == 12345u) fsum += 1.0;
+  }
+#endif
+#if SWARM_DIAG_EXTRA_VALU
+  {  // diagnostic: SWARM_DIAG_EXTRA_VALU dependent-free v_mul_f32 per wave
+    float z0 = px, z1 = py, z2 = pz, z3 = px + 1.f;
+#pragma unroll
+    for (int q = 0; q < SWARM_DIAG_EXTRA_VALU / 4; ++q) {
+      z0 = z0 * 0.999f; z1 = z1 * 0.999f; z2 = z2 * 0.999f; z3 = z3 * 0.999f;
+    }
+    if (z0 + z1 + z2 + z3 == 1234.5f) fsum += 1.0;
+  }
+#endif
   if (fast) h_pass1<true>(L, w, t, true, px, py, pz, A->P.ds_f, fsum, smin);
   else h_pass1<false>(L, w, t, act, px, py, pz, A->P.ds_f, fsum, smin);
   uint32_t ok[MSL];
