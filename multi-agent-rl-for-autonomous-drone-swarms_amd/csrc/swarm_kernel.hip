@@ -3328,10 +3328,14 @@ __device__ __forceinline__ void h_put(H256Lds& L, int w, int t, float x, float y
 
 // Lane t's two read bases into block b's planes (x / y and z / eligibility) as opaque LDS
 // addresses, so every rotation's read is an immediate offset of ds_read2_b32
-__device__ __forceinline__ void h_bases(H256Lds& L, int b, int t, s64_lds_cf*& P0, s64_lds_cf*& P1) {
-  P0 = (s64_lds_cf*)&L.seg[b][0][t];
-  P1 = (s64_lds_cf*)&L.seg[b][2][t];
+template <int NP>
+__device__ __forceinline__ void h_bases_p(float (*seg)[NP][H_BL], int b, int t, s64_lds_cf*& P0, s64_lds_cf*& P1) {
+  P0 = (s64_lds_cf*)&seg[b][0][t];
+  P1 = (s64_lds_cf*)&seg[b][2][t];
   asm volatile("" : "+v"(P0), "+v"(P1));
+}
+__device__ __forceinline__ void h_bases(H256Lds& L, int b, int t, s64_lds_cf*& P0, s64_lds_cf*& P1) {
+  h_bases_p<4>(L.seg, b, t, P0, P1);
 }
 // Traveling minima are kept as float bits and reduced with v_min_u32 (every value is a
 // non-negative float, whose bit patterns order like the floats): an integer min takes the
@@ -3474,14 +3478,15 @@ __device__ __forceinline__ void h_merge4(uint32_t (&k)[4], const uint32_t (&b)[4
   k[2] = min(c2, c3); k[3] = max(c2, c3);
 }
 
+// seg: the [block][x, y, z, eligibility][H_BL] planes; psum / pmn: the two handed-over sets
 template <bool FAST>
-__device__ __forceinline__ void h_pass1(H256Lds& L, int w, int t, bool self, float px, float py, float pz, float ds,
-                                        double& fsum, float& smin) {
+__device__ __forceinline__ void h_pass1(float (*seg)[4][H_BL], float (*psum)[H_N], float (*pmn)[H_N], int w, int t,
+                                        bool self, float px, float py, float pz, float ds, double& fsum, float& smin) {
   const int b1 = (w + 1) & 3, b2 = (w + 2) & 3;
   s64_lds_cf *A0, *A1, *B0, *B1, *C0, *C1;
-  h_bases(L, w, t, A0, A1);
-  h_bases(L, b1, t, B0, B1);
-  h_bases(L, b2, t, C0, C1);
+  h_bases_p(seg, w, t, A0, A1);
+  h_bases_p(seg, b1, t, B0, B1);
+  h_bases_p(seg, b2, t, C0, C1);
   float ta = 0.f, dummy = 0.f;
   uint32_t tam = 0x7f800000u, dummym = 0x7f800000u;
   // own block: rotations 31 .. 1 with the traveling mirror, then 32 from both sides
@@ -3503,10 +3508,10 @@ __device__ __forceinline__ void h_pass1(H256Lds& L, int w, int t, bool self, flo
     tc = wave_ror1(tc);
     tcm = wave_ror1_u(tcm);
   }
-  L.x.p1.sum[0][64 * b1 + t] = tb;
-  L.x.p1.mn[0][64 * b1 + t] = __uint_as_float(tbm);
-  L.x.p1.sum[1][64 * b2 + t] = tc;
-  L.x.p1.mn[1][64 * b2 + t] = __uint_as_float(tcm);
+  psum[0][64 * b1 + t] = tb;
+  pmn[0][64 * b1 + t] = __uint_as_float(tbm);
+  psum[1][64 * b2 + t] = tc;
+  pmn[1][64 * b2 + t] = __uint_as_float(tcm);
 }
 
 __device__ __forceinline__ void h_pass0(H256Lds& L, int w, int t, float px, float py, float pz, uint32_t keep,
@@ -3622,6 +3627,28 @@ __device__ __forceinline__ uint32_t h_finish_fast(const uint32_t (&nk)[4], const
 #else
 #define STAMP256(i) do {} while (0)
 #endif
+// swarm_step256s's LDS (the kernel is below, after swarm_step256)
+struct H256SLds {
+  float seg[4][4][H_BL];  // the step's planes (x, y, z, eligibility), as H256Lds
+  float4 ring[H_N];
+  float4 obst[H_MMAX];
+  float osoa[3 * H_MMAX];
+  uint32_t red[4];
+  struct {
+    float sum[2][H_N];
+    float mn[2][H_N];
+  } p1;
+  // the next episode: x / y / z planes (every new drone is active: no eligibility plane)
+  float sseg[4][3][H_BL];
+  float4 sring[H_N];
+  float4 sobst[H_MMAX];
+  float sosoa[3 * H_MMAX];
+  float4 sgoal;
+  uint32_t keys[2][4][H_N];  // key lists handed to another wave's drones (the next episode's pass,
+                             // then a continuing env's pass after the decision)
+};
+static_assert(sizeof(H256SLds) * 4 <= 160 * 1024, "four 512-thread workgroups per CU");
+
 #if SWARM_HAS_PART(7)  // emitted in its own translation unit only
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) swarm_step256(const S64Args args) {
   (void)args;  // read through s64_args()
@@ -3717,8 +3744,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     if (z0 + z1 + z2 + z3 == 1234.5f) fsum += 1.0;
   }
 #endif
-  if (fast) h_pass1<true>(L, w, t, true, px, py, pz, A->P.ds_f, fsum, smin);
-  else h_pass1<false>(L, w, t, act, px, py, pz, A->P.ds_f, fsum, smin);
+  if (fast) h_pass1<true>(L.seg, L.x.p1.sum, L.x.p1.mn, w, t, true, px, py, pz, A->P.ds_f, fsum, smin);
+  else h_pass1<false>(L.seg, L.x.p1.sum, L.x.p1.mn, w, t, act, px, py, pz, A->P.ds_f, fsum, smin);
   uint32_t ok[MSL];
 #pragma unroll
   for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
@@ -3906,6 +3933,337 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   }
 #endif
 }
+
+// ---- step256 with next-episode waves: one env per 512-thread workgroup
+// A reset is deterministic before the step decides it: the next episode's drones, obstacles and
+// goal are Philox4x32-10(seed, global env, episode + 1) draws (drone_swarm_env.py:65-90).  Waves
+// 0-3 step the env as swarm_step256 does (integrate, the formation / minimum pass, rewards and
+// terminations); waves 4-7 meanwhile draw the next episode and run its keys pass, obstacle keys
+// and exact finish, so a resetting env's observation is ready when the reset is decided and the
+// two halves of a resetting env's work (at N = 256 with the default radii, nearly every env every
+// step) run side by side instead of one after the other, at 8 waves per SIMD instead of 4.  A
+// continuing env's keys pass still runs after the decision, on waves 0-3 (as in swarm_step256).
+// Every output is the one swarm_step256 writes, bit for bit (same helpers, same order per drone).
+
+// h_pass0 over a given plane set, handing the other waves' lists through `keys`
+template <int NP>
+__device__ __forceinline__ void hs_pass0(float (*seg)[NP][H_BL], uint32_t (*keys)[4][H_N], int w, int t, float px,
+                                         float py, float pz, uint32_t keep, uint32_t (&nk)[4]) {
+  const int b1 = (w + 1) & 3, b2 = (w + 2) & 3;
+  const uint32_t t4 = (uint32_t)t << 2;
+  uint32_t kb[4], kc[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) { kb[s] = KEY_EMPTY; kc[s] = KEY_EMPTY; }
+  s64_lds_cf *A0, *A1, *B0, *B1, *C0, *C1;
+  h_bases_p<NP>(seg, w, t, A0, A1);
+  h_bases_p<NP>(seg, b1, t, B0, B1);
+  h_bases_p<NP>(seg, b2, t, C0, C1);
+  h_seg0<31, 1, 0, 0, true>(A0, A1, t4, px, py, pz, keep, nk, nk);
+  h_seg0<32, 32, 0, 0, false>(A0, A1, t4, px, py, pz, keep, nk, nk);
+  h_seg0<63, 0, 64, 192, true>(B0, B1, t4, px, py, pz, keep, nk, kb);
+  if (w < 2)
+    h_seg0<31, 0, 128, 128, true>(C0, C1, t4, px, py, pz, keep, nk, kc);
+  else
+    h_seg0<32, 1, 128, 128, true>(C0, C1, t4, px, py, pz, keep, nk, kc);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    keys[0][s][64 * b1 + t] = kb[s];
+    keys[1][s][64 * b2 + t] = kc[s];
+  }
+}
+// after the barrier: merge the two handed-over lists of drone i = 64 w + t, decode the codes
+__device__ __forceinline__ void hs_merge(uint32_t (*keys)[4][H_N], int i, int w, int t, uint32_t keep,
+                                         uint32_t (&nk)[4]) {
+  uint32_t kb[4], kc[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) { kb[s] = keys[0][s][i]; kc[s] = keys[1][s][i]; }
+  h_merge4(nk, kb);
+  h_merge4(nk, kc);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) nk[s] = h_decode(nk[s], w, t, keep);
+}
+// the exact top-K of the emitted observation (swarm_step256's finish)
+__device__ __forceinline__ void hs_finish(S64ArgPtr A, const float4* __restrict__ ring, const float4* __restrict__ obst,
+                                          int i, int M, const uint32_t (&nk)[4], const uint32_t (&ok)[5], float px,
+                                          float py, float pz, float (&wd)[4], int (&wj)[4], float (&od)[5],
+                                          int (&oj)[5]) {
+  constexpr int KS = H_K + 1, MSL = H_MS + 1;
+  const uint32_t ff = h_finish_fast(nk, ok, ring, obst, M, A->P.nb_keep, A->P.ob_keep, px, py, pz, wd, wj, od, oj);
+  if (__ballot(ff != 0) != 0) {
+    bool slow_nb, slow_ob;
+    s64_finish_general<KS, MSL, H_N, false, H_MMAX>(ff, nk, ok, ring, obst, i, M, A->P.nb_keep, A->P.ob_keep, false,
+                                                    px, py, pz, wd, wj, od, oj, slow_nb, slow_ob);
+    if (slow_nb) exact_select<KS, false>(ring, H_N, i, H_K, max_first(wd, H_K), px, py, pz, wd, wj);
+    if (slow_ob) exact_select<MSL, true>(obst, M, -1, H_MS, max_first(od, H_MS), px, py, pz, od, oj);
+  }
+}
+// state write-back + global state + observation row of drone i (swarm_step256's, in its order)
+__device__ __forceinline__ void hs_emit(S64ArgPtr A, int env, int i, int M, const float4* __restrict__ ring,
+                                        const float4* __restrict__ obst, const float (&wd)[4], const int (&wj)[4],
+                                        const float (&od)[5], const int (&oj)[5], float px, float py, float pz,
+                                        float vx, float vy, float vz, float gx, float gy, float gz, bool new_act,
+                                        bool do_reset, int new_step, uint32_t episode_new) {
+  const size_t ag = (size_t)env * H_N + i;
+  A->S.pos[ag * 3] = px; A->S.pos[ag * 3 + 1] = py; A->S.pos[ag * 3 + 2] = pz;
+  A->S.vel[ag * 3] = vx; A->S.vel[ag * 3 + 1] = vy; A->S.vel[ag * 3 + 2] = vz;
+  A->S.active[ag] = new_act ? 1 : 0;
+  if (i == 0) {
+    A->S.step_count[env] = do_reset ? 0 : new_step;
+    if (do_reset) {
+      A->S.episode[env] = episode_new;
+      A->S.goal[3 * env] = gx; A->S.goal[3 * env + 1] = gy; A->S.goal[3 * env + 2] = gz;
+    }
+  }
+  if (do_reset && i < M) {
+    float* o = A->S.obstacles + ((size_t)env * M + i) * 3;
+    const float4 q = obst[i];
+    o[0] = q.x; o[1] = q.y; o[2] = q.z;
+  }
+  if (A->O.global_state) {
+    float* gs = A->O.global_state + (size_t)env * (6 * H_N + 3);
+    gs[3 * i] = px; gs[3 * i + 1] = py; gs[3 * i + 2] = pz;
+    gs[3 * H_N + 3 * i] = vx; gs[3 * H_N + 3 * i + 1] = vy; gs[3 * H_N + 3 * i + 2] = vz;
+    if (i == 0) { gs[6 * H_N] = gx; gs[6 * H_N + 1] = gy; gs[6 * H_N + 2] = gz; }
+  }
+  float* row = A->O.obs + ag * (9 + 4 * H_K + 4 * H_MS);
+  row[0] = px; row[1] = py; row[2] = pz;
+  row[3] = vx; row[4] = vy; row[5] = vz;
+  row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
+#pragma unroll
+  for (int s = 0; s < H_K; ++s) {
+    const float4 q = lds_f4(ring + (wj[s] & (H_N - 1)));
+    row[9 + 4 * s] = q.x - px; row[10 + 4 * s] = q.y - py; row[11 + 4 * s] = q.z - pz; row[12 + 4 * s] = wd[s];
+  }
+#pragma unroll
+  for (int s = 0; s < H_MS; ++s) {
+    const float4 q = lds_f4(obst + (oj[s] & (H_MMAX - 1)));
+    row[21 + 4 * s] = q.x - px; row[22 + 4 * s] = q.y - py; row[23 + 4 * s] = q.z - pz; row[24 + 4 * s] = od[s];
+  }
+}
+
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) swarm_step256s(const S64Args args) {
+  (void)args;  // read through s64_args()
+  constexpr int MSL = H_MS + 1;
+  __shared__ H256SLds L;
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const bool spec = wv >= 4;           // waves 4-7: the next episode
+  const int w = wv & 3, t = threadIdx.x & 63;
+  const int i = 64 * w + t;            // drone
+  S64ArgPtr A = s64_args();
+  const int env = blockIdx.x;
+  if (env >= A->P.E) return;  // whole block
+  if (spec && !A->P.auto_reset) return;  // no reset can follow: nothing to prepare
+  const int M = A->P.M;
+  const size_t ag = (size_t)env * H_N + i;
+  const int stepc = A->S.step_count[env];
+  const uint32_t episode0 = A->S.episode[env];
+
+  if (spec) {
+    // ---- the next episode: draws (swarm_step256's reset block), planes, obstacles, goal
+    const uint32_t episode_new = episode0 + 1u;
+    const long long genv = A->P.env_offset + env;
+    float px, py, pz;
+    {
+      uint32_t wd4[4], wo[4];
+      draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)i, wd4);
+      const bool drawer = i <= M;  // obstacle i (i < M) or the goal (i == M)
+      if (drawer) draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)(H_N + i), wo);
+      const float lo_w = A->P.neg_half_w, wd_w = A->P.width_w;
+      px = uni(wd4[0], lo_w, wd_w);
+      py = uni(wd4[1], lo_w, wd_w);
+      pz = uni(wd4[2], lo_w, wd_w);
+      if (drawer) {
+        const float ox = uni(wo[0], lo_w, wd_w), oy = uni(wo[1], lo_w, wd_w), oz = uni(wo[2], lo_w, wd_w);
+        if (i < M) {
+          L.sobst[i] = make_float4(ox, oy, oz, 0.f);
+          L.sosoa[i] = ox; L.sosoa[H_MMAX + i] = oy; L.sosoa[2 * H_MMAX + i] = oz;
+        } else {
+          L.sgoal = make_float4(ox, oy, oz, 0.f);
+        }
+      }
+      L.sseg[w][0][t] = px; L.sseg[w][0][t + 64] = px;
+      L.sseg[w][1][t] = py; L.sseg[w][1][t + 64] = py;
+      L.sseg[w][2][t] = pz; L.sseg[w][2][t + 64] = pz;
+      L.sring[i] = make_float4(px, py, pz, 1.f);
+    }
+    const int n_active = __syncthreads_count(false);  // barrier 1 (the step's active count)
+    (void)__syncthreads_and(true);                     // barrier 2: the next episode's planes are in
+    A = s64_args();
+    uint32_t nk[4], ok[MSL];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) nk[s] = KEY_EMPTY;
+#pragma unroll
+    for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
+    bool c2 = false;
+    obstacle_pass_s64<MSL, false>(L.sosoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
+    hs_pass0<3>(L.sseg, L.keys, w, t, px, py, pz, A->P.nb_keep, nk);
+    __syncthreads();  // barrier 3: handed-over key lists written
+    A = s64_args();
+    hs_merge(L.keys, i, w, t, A->P.nb_keep, nk);
+    float wd[4], od[MSL];
+    int wj[4], oj[MSL];
+    hs_finish(A, L.sring, L.sobst, i, M, nk, ok, px, py, pz, wd, wj, od, oj);
+    __syncthreads();  // barrier 4: the step's votes are in (and every read of `keys` is done)
+    A = s64_args();
+    const uint32_t votes = L.red[0] | L.red[1] | L.red[2] | L.red[3];
+    const bool any_c = (votes & 1u) != 0, any_cand = (votes & 2u) != 0;
+    bool term_all = false, trunc_all = false;
+    if (n_active == 0) {
+      term_all = true;
+    } else {
+      const bool tl = stepc + 1 >= A->P.max_steps;
+      term_all = (!any_cand && !any_c && !tl) || any_c;
+      trunc_all = tl && !term_all;
+    }
+    if (!(term_all || trunc_all)) return;  // a continuing env: waves 0-3 emit it
+    const float4 g4 = L.sgoal;
+    hs_emit(A, env, i, M, L.sring, L.sobst, wd, wj, od, oj, px, py, pz, 0.f, 0.f, 0.f, g4.x, g4.y, g4.z, true, true, 0,
+            episode_new);
+    return;
+  }
+
+  // ---- waves 0-3: the step (swarm_step256's phases up to the reset decision)
+  const float gx = A->S.goal[3 * env], gy = A->S.goal[3 * env + 1], gz = A->S.goal[3 * env + 2];
+  float ax = A->actions[ag * 3], ay = A->actions[ag * 3 + 1], az = A->actions[ag * 3 + 2];
+  float px = A->S.pos[ag * 3], py = A->S.pos[ag * 3 + 1], pz = A->S.pos[ag * 3 + 2];
+  float vx = A->S.vel[ag * 3], vy = A->S.vel[ag * 3 + 1], vz = A->S.vel[ag * 3 + 2];
+  bool act = A->S.active[ag] != 0;
+  const bool has = A->amask == nullptr || A->amask[ag] != 0;
+  if (i < M) {
+    const float* o = A->S.obstacles + ((size_t)env * M + i) * 3;
+    const float ox = o[0], oy = o[1], oz = o[2];
+    L.obst[i] = make_float4(ox, oy, oz, 0.f);
+    L.osoa[i] = ox; L.osoa[H_MMAX + i] = oy; L.osoa[2 * H_MMAX + i] = oz;
+  }
+  const int n_active = __syncthreads_count(act);  // barrier 1
+  A = s64_args();
+  float prev_d = 0.f;
+  if (act) {
+    prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
+    if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
+    ax = clampf(ax, -1.f, 1.f) * A->P.amax;
+    ay = clampf(ay, -1.f, 1.f) * A->P.amax;
+    az = clampf(az, -1.f, 1.f) * A->P.amax;
+    vx = vx + ax * A->P.dt;
+    vy = vy + ay * A->P.dt;
+    vz = vz + az * A->P.dt;
+    const float s_sp = sqsum_1d(vx, vy, vz);
+    if (!(s_sp <= A->P.s_vmax)) {
+      const float sp = sqrt_rn(s_sp);
+      if (!(sp <= A->P.vmax || sp < (float)1e-8)) {
+        vx = (vx / sp) * A->P.vmax;
+        vy = (vy / sp) * A->P.vmax;
+        vz = (vz / sp) * A->P.vmax;
+      }
+    }
+    px = px + vx * A->P.dt;
+    py = py + vy * A->P.dt;
+    pz = pz + vz * A->P.dt;
+  }
+  if (n_active > 0) {
+    px = clampf(px, A->P.neg_half_w, A->P.half_w);
+    py = clampf(py, A->P.neg_half_w, A->P.half_w);
+    pz = clampf(pz, A->P.neg_half_w, A->P.half_w);
+  }
+  {
+    const float el = act ? 1.f : 0.f;
+    L.seg[w][0][t] = px; L.seg[w][0][t + 64] = px;
+    L.seg[w][1][t] = py; L.seg[w][1][t + 64] = py;
+    L.seg[w][2][t] = pz; L.seg[w][2][t + 64] = pz;
+    L.seg[w][3][t] = el; L.seg[w][3][t + 64] = el;
+    L.ring[i] = make_float4(px, py, pz, el);
+  }
+  const bool fast = __syncthreads_and(act) != 0;  // barrier 2
+  A = s64_args();
+
+  // ---- formation + minimum pass (every pair once), obstacle pass (swarm_step256's)
+  double fsum = 0.0;
+  float smin = __builtin_inff();
+  if (fast) h_pass1<true>(L.seg, L.p1.sum, L.p1.mn, w, t, true, px, py, pz, A->P.ds_f, fsum, smin);
+  else h_pass1<false>(L.seg, L.p1.sum, L.p1.mn, w, t, act, px, py, pz, A->P.ds_f, fsum, smin);
+  uint32_t ok[MSL];
+#pragma unroll
+  for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
+  bool ocoll = false;
+  obstacle_pass_s64<MSL, true>(L.osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
+  __syncthreads();  // barrier 3: handed-over sums / minima written
+  fsum += (double)L.p1.sum[0][i];
+  fsum += (double)L.p1.sum[1][i];
+  smin = fminf(smin, fminf(L.p1.mn[0][i], L.p1.mn[1][i]));
+  A = s64_args();
+
+  // ---- rewards / terminations: drone_swarm_env.py:120-172 (swarm_step256's)
+  bool pcoll = smin <= A->P.thr_pair * FAST_LO;
+  if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act)
+    pcoll = exact_pair_collision(L.ring, H_N, i, px, py, pz, A->P.s_pair);
+  const float curr = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
+  float rew = 0.f;
+  bool reached = false, collided = false, term = false, trunc = false, cont = false;
+  bool term_all = false, trunc_all = false;
+  int new_step = stepc;
+  bool p_coll = false, p_cand = false;
+  if (act) {
+    reached = (double)curr <= A->P.goal_radius;
+    collided = ocoll || pcoll;
+    p_coll = collided;
+    p_cand = !reached && !collided;
+    double r = ((double)prev_d - (double)curr) * A->P.kp;
+    if (n_active > 1) r = r + (-A->P.kf) * (fsum * inv_count(n_active - 1));
+    if (reached) r = r + A->P.r_goal;
+    if (collided) r = r + A->P.r_col;
+    rew = (float)r;
+  }
+  {
+    const bool wc = __ballot(p_coll) != 0, wdv = __ballot(p_cand) != 0;
+    if (t == 0) L.red[w] = (wc ? 1u : 0u) | (wdv ? 2u : 0u);
+  }
+  __syncthreads();  // barrier 4
+  const uint32_t votes = L.red[0] | L.red[1] | L.red[2] | L.red[3];
+  const bool any_c = (votes & 1u) != 0, any_cand = (votes & 2u) != 0;
+  A = s64_args();
+  if (n_active == 0) {
+    term_all = true;
+  } else {
+    new_step = stepc + 1;
+    const bool tl = new_step >= A->P.max_steps;
+    term_all = (!any_cand && !any_c && !tl) || any_c;
+    trunc_all = tl && !term_all;
+    if (act) {
+      const bool done_i = reached || collided;
+      term = done_i;
+      trunc = tl && !done_i;
+      cont = !done_i && !tl && !any_c;
+    }
+  }
+  const bool do_reset = A->P.auto_reset && (term_all || trunc_all);
+  A->O.reward[ag] = rew;
+  A->O.terminated[ag] = term ? 1 : 0;
+  A->O.truncated[ag] = trunc ? 1 : 0;
+  if (A->O.dist_goal) A->O.dist_goal[ag] = curr;
+  if (A->O.info_flags)
+    A->O.info_flags[ag] = (uint8_t)((act ? SWARM_AGENT_STEPPED : 0u) | (act && reached ? SWARM_AGENT_REACHED : 0u) |
+                                    (act && collided ? SWARM_AGENT_COLLISION : 0u) | (cont ? SWARM_AGENT_HAS_OBS : 0u));
+  if (i == 0)
+    A->O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
+                                   (do_reset ? SWARM_ENV_RESET : 0u));
+  if (do_reset) return;  // waves 4-7 emit the next episode
+
+  // ---- a continuing env (or no auto-reset): its keys pass on the emitted positions, then the
+  // finish and the write-back (waves 4-7 have left or are leaving: the barrier counts waves 0-3)
+  uint32_t nk[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) nk[s] = KEY_EMPTY;
+  hs_pass0<4>(L.seg, L.keys, w, t, px, py, pz, A->P.nb_keep, nk);
+  __syncthreads();  // barrier 5 (waves 0-3)
+  A = s64_args();
+  hs_merge(L.keys, i, w, t, A->P.nb_keep, nk);
+  float wd[4], od[MSL];
+  int wj[4], oj[MSL];
+  hs_finish(A, L.ring, L.obst, i, M, nk, ok, px, py, pz, wd, wj, od, oj);
+  A = s64_args();
+  hs_emit(A, env, i, M, L.ring, L.obst, wd, wj, od, oj, px, py, pz, vx, vy, vz, gx, gy, gz, cont, false, new_step,
+          episode0);
+}
 #endif
 
 // ------------------------------------------------------------------ host side
@@ -3961,8 +4319,10 @@ __attribute__((visibility("hidden"))) void* swarm_pick_step64_eval();
 __attribute__((visibility("hidden"))) void* swarm_pick_step16q();
 // the config-5 specialisation (SWARM_PART 7)
 __attribute__((visibility("hidden"))) void* swarm_pick_step256();
+__attribute__((visibility("hidden"))) void* swarm_pick_step256s();  // 512-thread, next-episode waves
 #if SWARM_HAS_PART(7)
 __attribute__((visibility("hidden"))) void* swarm_pick_step256() { return reinterpret_cast<void*>(swarm_step256); }
+__attribute__((visibility("hidden"))) void* swarm_pick_step256s() { return reinterpret_cast<void*>(swarm_step256s); }
 #endif
 #if SWARM_HAS_PART(6)
 __attribute__((visibility("hidden"))) void* swarm_pick_step16q() {
@@ -4062,6 +4422,15 @@ bool step16q_applies(const swarm_params_t* p, const KParams& k) {
 }
 
 // The config-5 specialisation swarm_step256 covers N = 256, K = 3, Ms = 4, 4 <= M <= 16, kinematic.
+// diagnostic: SWARM_STEP256_SPEC=1 selects swarm_step256s (512 threads: the step on waves 0-3,
+// the next episode on waves 4-7; measured slower, r05c) instead of swarm_step256 (read once)
+bool step256_spec() {
+  static const bool on = []() {
+    const char* v = getenv("SWARM_STEP256_SPEC");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
 bool step256_applies(const swarm_params_t* p, const KParams& k) {
   return p->kernel_path == SWARM_PATH_AUTO && k.N == H_N && k.K == H_K && k.Ms == H_MS && k.M >= H_MS &&
          k.M <= H_MMAX && p->dynamics == DYN_KIN;
@@ -4320,8 +4689,12 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   }
   if (mode == MODE_STEP && step256_applies(p, kp) && !s->env_cfg) {
     const S64Args args{kp, *s, actions, amask, *o};
-    hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step256()), dim3(kp.E), dim3(H_N), 0,
-                       (hipStream_t)stream, args);
+    if (step256_spec())
+      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step256s()), dim3(kp.E), dim3(2 * H_N), 0,
+                         (hipStream_t)stream, args);
+    else
+      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step256()), dim3(kp.E), dim3(H_N), 0,
+                         (hipStream_t)stream, args);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SWARM_OK;
@@ -4466,12 +4839,12 @@ int swarm_query_launch(const swarm_params_t* p, swarm_launch_info_t* info) {
     info->staged_obs = 0;
     info->kernel_id = SWARM_KERNEL_STEP16Q;
   }
-  if (rc == SWARM_OK && step256_applies(p, kp)) {  // one env per 256-thread workgroup, one lane per drone
+  if (rc == SWARM_OK && step256_applies(p, kp)) {  // one env per workgroup, one lane per drone (+ next-episode waves)
     info->lanes_per_env = H_N;
-    info->threads_per_block = H_N;
+    info->threads_per_block = step256_spec() ? 2 * H_N : H_N;
     info->envs_per_block = 1;
     info->blocks = kp.E;
-    info->lds_bytes = (int)sizeof(H256Lds);
+    info->lds_bytes = step256_spec() ? (int)sizeof(H256SLds) : (int)sizeof(H256Lds);
     info->staged_obs = 0;
     info->kernel_id = SWARM_KERNEL_STEP256;
   }
