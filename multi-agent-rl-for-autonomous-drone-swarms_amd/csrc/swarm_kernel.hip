@@ -2835,6 +2835,185 @@ __device__ __forceinline__ void q16_pair_pass(const float* __restrict__ soa, int
   }
 }
 
+// step16q's exact top-K of the emitted observation: quarter q measures neighbour slot q (q < 3)
+// and obstacle slot q; near-ties / unproven bounds take the quad-parallel exact selection.
+// dkey: the neighbour keys rank by d~ (PASS 1) instead of s' (PASS 0, a new episode's keys).
+__device__ __forceinline__ void q16_finish(S64ArgPtr A, Q16Lds& L, int d, int q, int M, const uint32_t (&nk)[Q_K + 1],
+                                           const uint32_t (&ok)[Q_MS + 1], bool dkey, float px, float py, float pz,
+                                           float& nd, float& ndx, float& ndy, float& ndz, float& od, float& odx,
+                                           float& ody, float& odz) {
+  constexpr int KS = Q_K + 1, MSL = Q_MS + 1;
+  const uint32_t nim = ~A->P.nb_keep, oim = ~A->P.ob_keep;
+  {
+    bool near_nb = false, near_ob = false;
+#pragma unroll
+    for (int s = 0; s + 1 < KS; ++s)
+      near_nb = near_nb | (__uint_as_float(nk[s + 1] & A->P.nb_keep) <=
+                           __uint_as_float((nk[s] & A->P.nb_keep) | nim) * FAST_HI);
+#pragma unroll
+    for (int s = 0; s + 1 < MSL; ++s)
+      near_ob = near_ob | ((ok[s + 1] != KEY_EMPTY) & (__uint_as_float(ok[s + 1] & A->P.ob_keep) <=
+                                                       __uint_as_float((ok[s] & A->P.ob_keep) | oim) * FAST_HI));
+    // this quarter's slots (q = 3 has no neighbour slot: it repeats slot 2, unused)
+    const uint32_t kn = q == 0 ? nk[0] : (q == 1 ? nk[1] : nk[2]);
+    const int jn = (d + (int)(kn & nim)) & (Q_N - 1);
+    const float4 qn = lds_f4(L.ring + jn);
+    ndx = qn.x - px; ndy = qn.y - py; ndz = qn.z - pz;
+    nd = sqrt_rn(sqsum_1d(ndx, ndy, ndz));
+    const uint32_t ko = q == 0 ? ok[0] : (q == 1 ? ok[1] : (q == 2 ? ok[2] : ok[3]));
+    const int jo = (int)(ko & oim) & (Q_MMAX - 1);
+    const float4 qo = lds_f4(L.obst + jo);
+    odx = qo.x - px; ody = qo.y - py; odz = qo.z - pz;
+    od = sqrt_rn(sqsum_f(odx, ody, odz));
+    // survivor bounds (finish_keys' tails) with slot K-1 / Ms-1 from quarters 2 / 3
+    const float w2 = quad_bcast<2>(nd), w3 = quad_bcast<3>(od);
+    const float nb_base = __uint_as_float(nk[Q_K] & A->P.nb_keep) * FAST_LO;
+    const bool ok_nb = dkey ? nb_base > w2 : nb_base > (w2 * w2) * FAST_HI;
+    const uint32_t last = ok[Q_MS];
+    const bool ok_ob = last == KEY_EMPTY || (int)(last & oim) >= M ||
+                       __uint_as_float(last & A->P.ob_keep) > (w3 * w3) * FAST_HI;
+    // rare (near-ties, unproven bounds): an exact selection split over the quad — quarter q
+    // measures neighbours d + q + 1 + 4i (obstacles q + 4i) exactly, then two DPP merges (what
+    // exact_select does serially, in the reference's (distance, index) order); each side alone
+    if (__ballot(near_nb || !ok_nb) != 0) {
+      q16_key k4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = q + 1 + 4 * i;
+        const int j = (d + r) & (Q_N - 1);
+        const float4 pj = lds_f4(L.ring + j);
+        const float dj = sqrt_rn(sqsum_1d(pj.x - px, pj.y - py, pj.z - pz));
+        k4[i] = r < Q_N ? ((q16_key)__float_as_uint(dj) << 32) | (uint32_t)j : ~0ull;
+      }
+      q16_quad_select4(k4);
+      const q16_key k2 = q == 0 ? k4[0] : (q == 1 ? k4[1] : k4[2]);
+      nd = __uint_as_float((uint32_t)(k2 >> 32));
+      const float4 qn2 = lds_f4(L.ring + ((int)k2 & (Q_N - 1)));
+      ndx = qn2.x - px; ndy = qn2.y - py; ndz = qn2.z - pz;
+    }
+    if (__ballot(near_ob || !ok_ob) != 0) {
+      q16_key k4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = q + 4 * i;
+        const float4 om = lds_f4(L.obst + m);
+        const float dm = sqrt_rn(sqsum_f(om.x - px, om.y - py, om.z - pz));
+        k4[i] = m < M ? ((q16_key)__float_as_uint(dm) << 32) | (uint32_t)m : ~0ull;
+      }
+      q16_quad_select4(k4);
+      const q16_key k2 = q == 0 ? k4[0] : (q == 1 ? k4[1] : (q == 2 ? k4[2] : k4[3]));
+      od = __uint_as_float((uint32_t)(k2 >> 32));
+      const float4 qo2 = lds_f4(L.obst + ((int)k2 & (Q_MMAX - 1)));
+      odx = qo2.x - px; ody = qo2.y - py; odz = qo2.z - pz;
+    }
+  }
+}
+
+// step16q's observation rows [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)]: the lanes' pieces
+// into the LDS stage (aliasing the dead rings: every ring / obstacle read is issued before), then,
+// by q16_store_obs, the env's block as 148 coalesced 16-B stores (whole 128-B lines)
+__device__ __forceinline__ void q16_stage_row(Q16Lds& L, int d, int q, float px, float py, float pz, float vx, float vy,
+                                              float vz, float gx, float gy, float gz, float nd, float ndx, float ndy,
+                                              float ndz, float od, float odx, float ody, float odz) {
+  wave_sync();
+  float* row = reinterpret_cast<float*>(L.stage) + d * Q_D;
+  if (q < 3) {
+    row[9 + 4 * q] = ndx; row[10 + 4 * q] = ndy; row[11 + 4 * q] = ndz; row[12 + 4 * q] = nd;
+  } else {
+    row[0] = px; row[1] = py; row[2] = pz;
+    row[3] = vx; row[4] = vy; row[5] = vz;
+    row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
+  }
+  row[21 + 4 * q] = odx; row[22 + 4 * q] = ody; row[23 + 4 * q] = odz; row[24 + 4 * q] = od;
+  wave_sync();
+}
+__device__ __forceinline__ void q16_store_obs(S64ArgPtr A, const Q16Lds& L, size_t ea, int lane) {
+  constexpr int V4 = Q_N * Q_D / 4;  // 148 float4: lanes take 64 + 64 + 20
+  const float4 v0 = L.stage[lane], v1 = L.stage[lane + 64];
+  const float4 v2 = L.stage[lane + 128 < V4 ? lane + 128 : V4 - 1];
+  float* ob = A->O.obs + ea * Q_D;  // 16-B aligned: 2,368 B per env
+  store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)lane, v0);
+  store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)(lane + 64), v1);
+  if (lane + 128 < V4) store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)(lane + 128), v2);
+}
+
+// step16q's next-episode wave (SWARM_STEP16Q 2-wave launch, wave 1 of an env's workgroup): a reset
+// is deterministic before the step decides it — Philox4x32-10(seed, global env, episode + 1) —
+// so while wave 0 steps the env, this wave draws the next episode exactly as step16q's reset block
+// does, runs its keys passes and exact finish and stages its observation rows.  At the decision
+// (one workgroup barrier) it writes the new episode's state, global state and observations when
+// the env resets, else it leaves.  The launch is latency-bound (one wave per SIMD): the reset's
+// work comes off the critical path of the resetting envs' waves.
+__device__ __forceinline__ void q16_next_episode(S64ArgPtr A, int env, int lane, Q16Lds& H,
+                                                 const uint32_t* decision) {
+  constexpr int MSL = Q_MS + 1;
+  const int d = lane >> 2, q = lane & 3;
+  const int M = A->P.M;
+  const size_t ea = (size_t)env * Q_N;
+  const size_t ag = ea + d;
+  const uint32_t episode_new = A->S.episode[env] + 1u;
+  const long long genv = A->P.env_offset + env;
+  const uint32_t blk = q < 2 ? (uint32_t)d : (q == 2 ? (uint32_t)(Q_N + d) : (uint32_t)(Q_N + M));
+  uint32_t wv[4];
+  draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, blk, wv);
+  const float lo_w = A->P.neg_half_w, wd_w = A->P.width_w;
+  const float ux = uni(wv[0], lo_w, wd_w), uy = uni(wv[1], lo_w, wd_w), uz = uni(wv[2], lo_w, wd_w);
+  const float px = quad_bcast<0>(ux), py = quad_bcast<0>(uy), pz = quad_bcast<0>(uz);
+  const float gx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ux), 3));
+  const float gy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(uy), 3));
+  const float gz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(uz), 3));
+  if (q == 2 && d < M) {
+    H.obst[d] = make_float4(ux, uy, uz, 0.f);
+    H.osoa[d] = ux; H.osoa[Q_MMAX + d] = uy; H.osoa[2 * Q_MMAX + d] = uz;
+  }
+  if (q == 0) {
+    H.ring[d] = make_float4(px, py, pz, 1.f);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      H.soa[d + 16 * c] = px; H.soa[32 + d + 16 * c] = py; H.soa[64 + d + 16 * c] = pz;
+      H.soa[96 + d + 16 * c] = 1.f;
+    }
+  }
+  wave_sync();
+  uint32_t nk[Q_K + 1], ok[MSL];
+#pragma unroll
+  for (int s = 0; s < Q_K + 1; ++s) nk[s] = KEY_EMPTY;
+#pragma unroll
+  for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
+  float s2 = 0.f, e2 = 0.f;
+  bool c2 = false;
+  q16_pair_pass<0, true>(H.soa, d, q, px, py, pz, true, A->P.nb_keep, 0.f, nk, s2, e2);
+  obstacle_pass_s64<MSL, false>(H.osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
+  float nd, ndx, ndy, ndz, od, odx, ody, odz;
+  q16_finish(A, H, d, q, M, nk, ok, false, px, py, pz, nd, ndx, ndy, ndz, od, odx, ody, odz);
+  q16_stage_row(H, d, q, px, py, pz, 0.f, 0.f, 0.f, gx, gy, gz, nd, ndx, ndy, ndz, od, odx, ody, odz);
+  __syncthreads();  // wave 0's decision
+  if (*reinterpret_cast<const volatile uint32_t*>(decision) == 0u) return;
+  A = s64_args();
+  if (q == 0) {
+    float* pe = A->S.pos + ag * 3;
+    float* ve = A->S.vel + ag * 3;
+    pe[0] = px; pe[1] = py; pe[2] = pz;
+    ve[0] = 0.f; ve[1] = 0.f; ve[2] = 0.f;
+  }
+  if (lane == 0) {
+    A->S.step_count[env] = 0;
+    A->S.episode[env] = episode_new;
+    A->S.goal[3 * env + 0] = gx; A->S.goal[3 * env + 1] = gy; A->S.goal[3 * env + 2] = gz;
+  }
+  if (q == 2 && d < M) {  // the obstacle this lane drew
+    float* o = A->S.obstacles + ((size_t)env * M + d) * 3;
+    o[0] = ux; o[1] = uy; o[2] = uz;
+  }
+  if (A->O.global_state && q == 0) {
+    float* gs = A->O.global_state + (size_t)env * (6 * Q_N + 3);
+    gs[3 * d] = px; gs[3 * d + 1] = py; gs[3 * d + 2] = pz;
+    gs[3 * Q_N + 3 * d] = 0.f; gs[3 * Q_N + 3 * d + 1] = 0.f; gs[3 * Q_N + 3 * d + 2] = 0.f;
+    if (d == 0) { gs[6 * Q_N + 0] = gx; gs[6 * Q_N + 1] = gy; gs[6 * Q_N + 2] = gz; }
+  }
+  q16_store_obs(A, H, ea, lane);
+}
+
 #ifdef SWARM_STAMPS
 #define Q16_FLAG(f) (q16_flags |= (f))  // slow paths a wave took (tools/stamps16.py)
 #else
@@ -2846,9 +3025,6 @@ __device__ __forceinline__ void q16_pair_pass(const float* __restrict__ soa, int
 // per-phase re-fetch; SWARM_LAT_REFETCH_ON=1 restores it here, diagnostics only).
 #ifndef SWARM_LAT_REFETCH_ON
 #define SWARM_LAT_REFETCH_ON 0
-#endif
-#ifndef SWARM_Q16_DIRECT_OBS
-#define SWARM_Q16_DIRECT_OBS 0
 #endif
 #ifndef SWARM_Q16_FLOOR
 #define SWARM_Q16_FLOOR 0
@@ -2862,17 +3038,27 @@ __device__ __forceinline__ void q16_pair_pass(const float* __restrict__ soa, int
 #ifndef SWARM_Q16_WAVES_PER_EU
 #define SWARM_Q16_WAVES_PER_EU 4
 #endif
-template <int G>
-__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(SWARM_Q16_WAVES_PER_EU)))
+// SPEC: one env per 2-wave workgroup, wave 1 running q16_next_episode (G must be 1)
+template <int G, bool SPEC = false>
+__global__ void __launch_bounds__(SPEC ? 128 : 64 * G) __attribute__((amdgpu_waves_per_eu(SWARM_Q16_WAVES_PER_EU)))
 swarm_step16q(const S64Args args) {
   (void)args;  // read through s64_args()
+  static_assert(!SPEC || G == 1, "the 2-wave launch holds one env per workgroup");
   constexpr int KS = Q_K + 1, MSL = Q_MS + 1;
-  __shared__ Q16Lds ldsq[G];
+  __shared__ Q16Lds ldsq[SPEC ? 2 : G];
+  __shared__ uint32_t decision;  // SPEC: wave 0's reset decision for wave 1
   const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int w = SPEC ? 0 : wv;
   S64ArgPtr A = s64_args();
   const int env = blockIdx.x * G + w;
-  if (env >= A->P.E) return;  // whole wave
+  if (env >= A->P.E) return;  // whole wave (workgroup)
+  if constexpr (SPEC) {
+    if (wv == 1) {
+      if (A->P.auto_reset) q16_next_episode(A, env, lane, ldsq[1], &decision);
+      return;
+    }
+  }
   Q16Lds& L = ldsq[w];
   const int d = lane >> 2, q = lane & 3;
   STAMP_AT(env, 0);
@@ -3069,7 +3255,27 @@ swarm_step16q(const S64Args args) {
   // ---- in-kernel auto-reset (wave-uniform): new episode, then its key passes
   uint32_t episode_new = episode0;
   bool dkey = true;
-  if (do_reset) {
+  if constexpr (SPEC) {
+    if (A->P.auto_reset) {
+      if (lane == 0) decision = do_reset ? 1u : 0u;
+      __syncthreads();  // wave 1 holds the next episode: it emits it when the env resets
+    }
+    if (do_reset) {  // this wave's remaining outputs: the terminated / truncated / active rows
+      s64_gu8* p_term = (s64_gu8*)A->O.terminated;
+      s64_gu8* p_trunc = (s64_gu8*)A->O.truncated;
+      s64_gu8* p_act = (s64_gu8*)A->S.active;
+      asm volatile("" : "+s"(p_term), "+s"(p_trunc), "+s"(p_act));
+      const int grp = lane >> 2;
+      if (grp < 3) {
+        const uint64_t m = grp == 0 ? m_term : (grp == 1 ? m_trunc : ~0ull);
+        const uint32_t nib = (uint32_t)(m >> (16 * (lane & 3)));
+        const uint32_t word = (nib & 1u) | ((nib >> 4) & 1u) << 8 | ((nib >> 8) & 1u) << 16 | ((nib >> 12) & 1u) << 24;
+        s64_gu8* base = grp == 0 ? p_term : (grp == 1 ? p_trunc : p_act);
+        *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(base + ea + 4 * (lane & 3)) = word;
+      }
+      return;
+    }
+  } else if (do_reset) {
     const long long genv = A->P.env_offset + env;
     episode_new = episode0 + 1u;
     Q16_FLAG(4u);
@@ -3110,73 +3316,8 @@ swarm_step16q(const S64Args args) {
   SWARM_LAT_REFETCH(A);
 
   // ---- exact top-K: quarter q finishes neighbour slot q (q < 3) and obstacle slot q
-  const uint32_t nim = ~A->P.nb_keep, oim = ~A->P.ob_keep;
-  float nd = 0.f, ndx = 0.f, ndy = 0.f, ndz = 0.f, od = 0.f, odx = 0.f, ody = 0.f, odz = 0.f;
-  {
-    bool near_nb = false, near_ob = false;
-#pragma unroll
-    for (int s = 0; s + 1 < KS; ++s)
-      near_nb = near_nb | (__uint_as_float(nk[s + 1] & A->P.nb_keep) <=
-                           __uint_as_float((nk[s] & A->P.nb_keep) | nim) * FAST_HI);
-#pragma unroll
-    for (int s = 0; s + 1 < MSL; ++s)
-      near_ob = near_ob | ((ok[s + 1] != KEY_EMPTY) & (__uint_as_float(ok[s + 1] & A->P.ob_keep) <=
-                                                       __uint_as_float((ok[s] & A->P.ob_keep) | oim) * FAST_HI));
-    // this quarter's slots (q = 3 has no neighbour slot: it repeats slot 2, unused)
-    const uint32_t kn = q == 0 ? nk[0] : (q == 1 ? nk[1] : nk[2]);
-    const int jn = (d + (int)(kn & nim)) & (Q_N - 1);
-    const float4 qn = lds_f4(L.ring + jn);
-    ndx = qn.x - px; ndy = qn.y - py; ndz = qn.z - pz;
-    nd = sqrt_rn(sqsum_1d(ndx, ndy, ndz));
-    const uint32_t ko = q == 0 ? ok[0] : (q == 1 ? ok[1] : (q == 2 ? ok[2] : ok[3]));
-    const int jo = (int)(ko & oim) & (Q_MMAX - 1);
-    const float4 qo = lds_f4(L.obst + jo);
-    odx = qo.x - px; ody = qo.y - py; odz = qo.z - pz;
-    od = sqrt_rn(sqsum_f(odx, ody, odz));
-    // survivor bounds (finish_keys' tails) with slot K-1 / Ms-1 from quarters 2 / 3
-    const float w2 = quad_bcast<2>(nd), w3 = quad_bcast<3>(od);
-    const float nb_base = __uint_as_float(nk[Q_K] & A->P.nb_keep) * FAST_LO;
-    const bool ok_nb = dkey ? nb_base > w2 : nb_base > (w2 * w2) * FAST_HI;
-    const uint32_t last = ok[Q_MS];
-    const bool ok_ob = last == KEY_EMPTY || (int)(last & oim) >= M ||
-                       __uint_as_float(last & A->P.ob_keep) > (w3 * w3) * FAST_HI;
-    // rare (near-ties, unproven bounds): an exact selection split over the quad — quarter q
-    // measures neighbours d + q + 1 + 4i (obstacles q + 4i) exactly, then two DPP merges (what
-    // exact_select does serially, in the reference's (distance, index) order); each side alone
-    if (__ballot(near_nb || !ok_nb) != 0) {
-      q16_key k4[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = q + 1 + 4 * i;
-        const int j = (d + r) & (Q_N - 1);
-        const float4 pj = lds_f4(L.ring + j);
-        const float dj = sqrt_rn(sqsum_1d(pj.x - px, pj.y - py, pj.z - pz));
-        k4[i] = r < Q_N ? ((q16_key)__float_as_uint(dj) << 32) | (uint32_t)j : ~0ull;
-      }
-      q16_quad_select4(k4);
-      const q16_key k2 = q == 0 ? k4[0] : (q == 1 ? k4[1] : k4[2]);
-      nd = __uint_as_float((uint32_t)(k2 >> 32));
-      const float4 qn2 = lds_f4(L.ring + ((int)k2 & (Q_N - 1)));
-      ndx = qn2.x - px; ndy = qn2.y - py; ndz = qn2.z - pz;
-      Q16_FLAG(1u);
-    }
-    if (__ballot(near_ob || !ok_ob) != 0) {
-      q16_key k4[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = q + 4 * i;
-        const float4 om = lds_f4(L.obst + m);
-        const float dm = sqrt_rn(sqsum_f(om.x - px, om.y - py, om.z - pz));
-        k4[i] = m < M ? ((q16_key)__float_as_uint(dm) << 32) | (uint32_t)m : ~0ull;
-      }
-      q16_quad_select4(k4);
-      const q16_key k2 = q == 0 ? k4[0] : (q == 1 ? k4[1] : (q == 2 ? k4[2] : k4[3]));
-      od = __uint_as_float((uint32_t)(k2 >> 32));
-      const float4 qo2 = lds_f4(L.obst + ((int)k2 & (Q_MMAX - 1)));
-      odx = qo2.x - px; ody = qo2.y - py; odz = qo2.z - pz;
-      Q16_FLAG(16u);
-    }
-  }
+  float nd, ndx, ndy, ndz, od, odx, ody, odz;
+  q16_finish(A, L, d, q, M, nk, ok, dkey, px, py, pz, nd, ndx, ndy, ndz, od, odx, ody, odz);
   STAMP_AT(env, 6);
   SWARM_LAT_REFETCH(A);
 
@@ -3226,34 +3367,9 @@ swarm_step16q(const S64Args args) {
   STAMP_AT(env, 7);
   SWARM_LAT_REFETCH(A);
 
-  // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)]: the lanes' pieces into
-  // the LDS stage (aliasing the dead rings), then the env's block as coalesced 16-B stores
-#if SWARM_Q16_DIRECT_OBS  // diagnostic: round 3's scattered dword stores straight from registers
-  float* row = A->O.obs + ag * Q_D;
-#else
-  wave_sync();  // every ring / obstacle read of the finish is issued before the stage overwrites them
-  float* row = reinterpret_cast<float*>(L.stage) + d * Q_D;
-#endif
-  if (q < 3) {
-    row[9 + 4 * q] = ndx; row[10 + 4 * q] = ndy; row[11 + 4 * q] = ndz; row[12 + 4 * q] = nd;
-  } else {
-    row[0] = px; row[1] = py; row[2] = pz;
-    row[3] = vx; row[4] = vy; row[5] = vz;
-    row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
-  }
-  row[21 + 4 * q] = odx; row[22 + 4 * q] = ody; row[23 + 4 * q] = odz; row[24 + 4 * q] = od;
-#if !SWARM_Q16_DIRECT_OBS
-  wave_sync();
-  {
-    constexpr int V4 = Q_N * Q_D / 4;  // 148 float4: lanes take 64 + 64 + 20
-    const float4 v0 = L.stage[lane], v1 = L.stage[lane + 64];
-    const float4 v2 = L.stage[lane + 128 < V4 ? lane + 128 : V4 - 1];
-    float* ob = A->O.obs + ea * Q_D;  // 16-B aligned: 2,368 B per env
-    store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)lane, v0);
-    store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)(lane + 64), v1);
-    if (lane + 128 < V4) store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)(lane + 128), v2);
-  }
-#endif
+  // ---- observation rows: staged in LDS, stored as coalesced 16-B stores
+  q16_stage_row(L, d, q, px, py, pz, vx, vy, vz, gx, gy, gz, nd, ndx, ndy, ndz, od, odx, ody, odz);
+  q16_store_obs(A, L, ea, lane);
   STAMP_AT(env, 8);
 #ifdef SWARM_STAMPS
   if (lane == 0 && env < (1 << 16)) g_stamps[env * 16 + 12] = __builtin_amdgcn_s_memrealtime();
@@ -4316,7 +4432,7 @@ SWARM_PICK_DECL(3);
 __attribute__((visibility("hidden"))) void* swarm_pick_step64(bool persistent, bool physics);
 __attribute__((visibility("hidden"))) void* swarm_pick_step64_eval();
 // the config-2 specialisation (SWARM_PART 6)
-__attribute__((visibility("hidden"))) void* swarm_pick_step16q();
+__attribute__((visibility("hidden"))) void* swarm_pick_step16q(bool spec);
 // the config-5 specialisation (SWARM_PART 7)
 __attribute__((visibility("hidden"))) void* swarm_pick_step256();
 __attribute__((visibility("hidden"))) void* swarm_pick_step256s();  // 512-thread, next-episode waves
@@ -4325,8 +4441,8 @@ __attribute__((visibility("hidden"))) void* swarm_pick_step256() { return reinte
 __attribute__((visibility("hidden"))) void* swarm_pick_step256s() { return reinterpret_cast<void*>(swarm_step256s); }
 #endif
 #if SWARM_HAS_PART(6)
-__attribute__((visibility("hidden"))) void* swarm_pick_step16q() {
-  return reinterpret_cast<void*>(swarm_step16q<Q_WG_ENVS>);
+__attribute__((visibility("hidden"))) void* swarm_pick_step16q(bool spec) {
+  return spec ? reinterpret_cast<void*>(swarm_step16q<1, true>) : reinterpret_cast<void*>(swarm_step16q<Q_WG_ENVS>);
 }
 #endif
 #if SWARM_HAS_PART(5)
@@ -4415,6 +4531,15 @@ bool step64_applies(const swarm_params_t* p, const KParams& k) {
          k.M <= S64_MMAX && (p->dynamics == DYN_KIN || p->dynamics == DYN_PHYS);
 }
 
+// step16q's 2-wave launch (the next episode prepared by a second wave) unless SWARM_STEP16Q_SPEC=0
+// selects the one-wave-per-env launch (read once per process)
+bool step16q_spec() {
+  static const bool on = []() {
+    const char* v = getenv("SWARM_STEP16Q_SPEC");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
 // The config-2 specialisation swarm_step16q covers N = 16, K = 3, Ms = 4, 4 <= M <= 16, kinematic.
 bool step16q_applies(const swarm_params_t* p, const KParams& k) {
   return p->kernel_path == SWARM_PATH_AUTO && k.N == Q_N && k.K == Q_K && k.Ms == Q_MS && k.M >= Q_MS &&
@@ -4681,8 +4806,12 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   if (mode == MODE_STEP && step16q_applies(p, kp) && !s->env_cfg && ((uintptr_t)o->obs) % 16 == 0 &&
       ((uintptr_t)o->terminated | (uintptr_t)o->truncated | (uintptr_t)s->active) % 4 == 0) {
     const S64Args args{kp, *s, actions, amask, *o, ev};
-    hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step16q()), dim3((kp.E + Q_WG_ENVS - 1) / Q_WG_ENVS),
-                       dim3(64 * Q_WG_ENVS), 0, (hipStream_t)stream, args);
+    if (step16q_spec())  // one env per 2-wave workgroup: wave 1 prepares the next episode
+      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step16q(true)), dim3(kp.E), dim3(128), 0,
+                         (hipStream_t)stream, args);
+    else
+      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step16q(false)),
+                         dim3((kp.E + Q_WG_ENVS - 1) / Q_WG_ENVS), dim3(64 * Q_WG_ENVS), 0, (hipStream_t)stream, args);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SWARM_OK;
@@ -4832,10 +4961,11 @@ int swarm_query_launch(const swarm_params_t* p, swarm_launch_info_t* info) {
   const int rc = build_kparams(p, &kp, info);
   if (rc == SWARM_OK && step16q_applies(p, kp)) {  // one env per 64-lane wave, 4 lanes per drone
     info->lanes_per_env = 64;
-    info->threads_per_block = 64 * Q_WG_ENVS;
-    info->envs_per_block = Q_WG_ENVS;
-    info->blocks = (kp.E + Q_WG_ENVS - 1) / Q_WG_ENVS;
-    info->lds_bytes = Q_WG_ENVS * (int)sizeof(Q16Lds);
+    const bool spec = step16q_spec();
+    info->threads_per_block = spec ? 128 : 64 * Q_WG_ENVS;
+    info->envs_per_block = spec ? 1 : Q_WG_ENVS;
+    info->blocks = spec ? kp.E : (kp.E + Q_WG_ENVS - 1) / Q_WG_ENVS;
+    info->lds_bytes = spec ? 2 * (int)sizeof(Q16Lds) + 4 : Q_WG_ENVS * (int)sizeof(Q16Lds);
     info->staged_obs = 0;
     info->kernel_id = SWARM_KERNEL_STEP16Q;
   }
