@@ -33,9 +33,6 @@ namespace {
 constexpr int EVAL_THREADS = 64;   // one wave per env
 constexpr int EVAL_WG_ENVS = 4;    // independent waves per workgroup: a quarter of the workgroups
                                    // to dispatch (8192 one-wave workgroups cost the dispatcher ~4 us)
-#ifndef SWARM_EVAL_ABLATE  // diagnostics (tools/): 1 = skip the formation error, 2 = skip episode
-#define SWARM_EVAL_ABLATE 0  // ends, 3 = no counter atomic (slot 0 of the segment), 4 = 1 + 2, 5 = return
-#endif                       // after the first loads
 constexpr int EVAL_MAX_N = 1024;
 
 __device__ __forceinline__ float norm1d(float x, float y, float z) {
@@ -161,9 +158,8 @@ __global__ void __launch_bounds__(EVAL_THREADS * EVAL_WG_ENVS) eval_update_kerne
   const double fe_sum0 = v.fe_sum[e];
   const int steps0 = v.ep_steps[e];
   const int reached0 = v.reached_step[e];
-  if (!(status & SWARM_EVAL_LIVE) || SWARM_EVAL_ABLATE == 5) return;
-  const bool ends = (done & (SWARM_ENV_TERMINATED | SWARM_ENV_TRUNCATED)) != 0 && SWARM_EVAL_ABLATE != 2 &&
-                    SWARM_EVAL_ABLATE != 4;
+  if (!(status & SWARM_EVAL_LIVE)) return;
+  const bool ends = (done & (SWARM_ENV_TERMINATED | SWARM_ENV_TRUNCATED)) != 0;
   const bool restarts = ends && (done & SWARM_ENV_RESET) != 0;
   // SWARM_EVAL_STEP_FUSED: the step launch (out.eval) already added this step's reward, steps,
   // reached step, collision vote and path lengths (swarm_kernel.hip s64_env, the same arithmetic):
@@ -245,8 +241,7 @@ __global__ void __launch_bounds__(EVAL_THREADS * EVAL_WG_ENVS) eval_update_kerne
   not_reached = __any(not_reached) ? 1 : 0;
   // ---- formation error of the observed set (evaluate_protocol.py:103-116)
   double fe = 0.0;
-  if (SWARM_EVAL_ABLATE == 1 || SWARM_EVAL_ABLATE == 4) {
-  } else if (n_obs > 1 && a.N == EVAL_THREADS) {
+  if (n_obs > 1 && a.N == EVAL_THREADS) {
     // one drone per lane: symmetric rotations.  At rotation r lane t measures the pair
     // (t, t+r); r = 1..31 covers every unordered pair except the 32 opposite ones once, r = 32
     // covers those twice (lanes t and t+32).  Distances are symmetric bit for bit (|a-b| = |b-a|
@@ -332,7 +327,7 @@ __global__ void __launch_bounds__(EVAL_THREADS * EVAL_WG_ENVS) eval_update_kerne
   const bool collided = coll || (status & SWARM_EVAL_COLLIDED);
   const long long genv = a.env_offset + e;
   const unsigned seg = (unsigned)(genv % SWARM_EVAL_SEGMENTS);
-  const unsigned k = SWARM_EVAL_ABLATE == 3 ? 0u : atomicAdd(v.count + seg, 1u);
+  const unsigned k = atomicAdd(v.count + seg, 1u);
   double* rec = record_slot(v, seg, k);
   if (rec) {
     rec[0] = (double)genv;  // global env index

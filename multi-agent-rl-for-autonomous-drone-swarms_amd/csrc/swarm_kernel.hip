@@ -48,60 +48,43 @@
 #endif
 #define SWARM_HAS_PART(k) (SWARM_PART == -1 || SWARM_PART == (k))
 #define SWARM_HAS_HOST (SWARM_PART == -1 || SWARM_PART == 4)
-
-// Diagnostic ablation switches (tools/ablate.sh builds variants; never set in the product build)
-#ifndef SWARM_ABLATE
-#define SWARM_ABLATE 0
-#endif
-#define ABL_PAIR 1     // skip the pair pass
-#define ABL_OBS 2      // skip the observation store
-#define ABL_FINISH 4   // skip the exact top-K re-ranking
-#define ABL_RESET 8    // never auto-reset
-#define ABL_OBST 16    // skip the obstacle pass
-#define ABL_W64 64     // one-team waves use the generic (rolled) pair pass
-#define ABL_STORE_ONLY 128  // step64: obs stores straight from registers (wrong values)
-#define ABL_STAGE_ONLY 256  // step64: obs staged through LDS, not stored
-#define ABL_ROW_ONLY 512    // step64: obs row computed, neither staged nor stored
-#define ABL_RESET_WORK 1024 // step64: a resetting env draws its new state but skips its key passes,
-                            // finish and obs (wrong obs; the dynamics are unchanged)
-#define ABL_EXACT 2048      // sqrt_rn = v_sqrt_f32 and the sdot norm in f32 (inexact; timing only)
-#define ABL_GENERAL 4096    // step64: never run the general finish (near-tie waves keep the fast answer)
-#define ABL_PHILOX 8192     // step64: reset draws from one multiply-xor per word instead of Philox
-#define ABL_EXSEL 16384     // step64: the general finish without exact_select (its answer kept)
-#define ABL_GENKEEP 32768   // step64: the fast finish's checks and ballot kept, the general finish skipped
-#define ABL_ROWGATHER 65536 // step64: the obs row's neighbour / obstacle columns without their LDS gathers (wrong values)
+// the generic kernel's instantiations (parts 0-3)
+#define SWARM_PARTS_GENERIC (SWARM_HAS_PART(0) || SWARM_HAS_PART(1) || SWARM_HAS_PART(2) || SWARM_HAS_PART(3))
 
 // Diagnostic phase timestamps (tools/stamps.py; never set in the product build)
-#ifdef SWARM_STAMPS
-__device__ unsigned long long g_stamps[1 << 20];
-#define STAMP_AT(rec, i)                                                                 \
-  do {                                                                                   \
-    __builtin_amdgcn_sched_barrier(0);                                                   \
-    unsigned long long ts_;                                                              \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");           \
-    __builtin_amdgcn_sched_barrier(0);                                                   \
-    if ((threadIdx.x & 63) == 0 && (rec) < (1 << 16)) g_stamps[(rec) * 16 + (i)] = ts_;           \
-  } while (0)
-#else
-#define STAMP_AT(rec, i) do {} while (0)
-#endif
-#define STAMP(i) STAMP_AT(blockIdx.x, i)
+#include "swarm_stamps.h"  // diagnostic phase stamps (empty unless -DSWARM_STAMPS)
 
-namespace {
+// Tuning constants (each measured against its alternatives)
+constexpr int FB_BATCH = 8;            // exact scans: LDS reads in flight per batch
+constexpr int S64_PAIR_BATCH = 4;      // step64 pair pass: rotations per scheduling group
+constexpr int S64_CH_ROWS = 32;        // step64 obs rows per LDS staging chunk
+constexpr int S64_WG_ENVS_C = 4;       // step64: one-env waves per workgroup
+constexpr int S64_EVAL_WAVES = 8;      // step64 with the fused eval: waves per EU
+[[maybe_unused]] constexpr int Q16_WAVES_PER_EU = 4;    // step16q register budget (71 VGPRs, no spills)
+constexpr int H_BATCH_C = 8;           // step256 passes: rotations per scheduling batch
+constexpr bool WT_STORES = true;       // obs rows as write-through (sc1) buffer stores
+constexpr int OBS_STORE_AUX = 16;      // their cache-policy bits (16 = sc1)
+
+// Device helpers (structs, constants, inline functions) live in namespace swarm_dev: inline functions
+// with external linkage, so a helper that one translation unit (SWARM_PART) does not use is neither
+// emitted nor warned about.  The kernels are in anonymous namespaces (each translation unit's own).
+namespace swarm_dev {}
+using namespace swarm_dev;
+namespace swarm_dev {
 
 constexpr uint32_t KEY_EMPTY = 0xffffffffu;
 constexpr int MODE_STEP = 0;
 constexpr int MODE_RESET = 1;
 constexpr int MODE_OBSERVE = 2;
 constexpr int KIND_STEP = 0;
-constexpr int KIND_AUX = 1;  // reset / observe
+[[maybe_unused]] constexpr int KIND_AUX = 1;  // reset / observe
 constexpr int DYN_KIN = SWARM_DYN_KINEMATIC;
 constexpr int DYN_PHYS = SWARM_DYN_POINTMASS_PHYSICS;
-constexpr int MAX_N = 1024;
-constexpr int MAX_K = 16;
-constexpr int MAX_MS = 16;
-constexpr int STAGE_BUDGET = 8 * 1024;  // bytes of LDS for one obs staging chunk
-constexpr int LDS_LIMIT = 160 * 1024;
+[[maybe_unused]] constexpr int MAX_N = 1024;
+[[maybe_unused]] constexpr int MAX_K = 16;
+[[maybe_unused]] constexpr int MAX_MS = 16;
+[[maybe_unused]] constexpr int STAGE_BUDGET = 8 * 1024;  // bytes of LDS for one obs staging chunk
+[[maybe_unused]] constexpr int LDS_LIMIT = 160 * 1024;
 constexpr float PAD_POS = 1e18f;        // position of padding lanes (t >= N): never a neighbour
 constexpr float FAST_LO = 1.0f - 0x1p-18f;  // |s' - s| <= 2^-21 s; bands use an 8x margin
 constexpr float FAST_HI = 1.0f + 0x1p-18f;
@@ -152,7 +135,6 @@ __device__ __forceinline__ int clamp_obstacles(int m, int M) { return m < 0 ? 0 
 // The fast path is OCML's own correction step without its input scaling (needed only below
 // 2^-96) and special-value fixup (inf/NaN/negative never occur here): bit-identical results.
 __device__ __forceinline__ float sqrt_rn(float x) {
-  if (SWARM_ABLATE & ABL_EXACT) return __builtin_amdgcn_sqrtf(x);
   if (__builtin_expect(__ballot(!(x >= 0x1p-96f || x == 0.0f)) != 0, 0)) return __builtin_sqrtf(x);
   float r = __builtin_amdgcn_sqrtf(x);  // v_sqrt_f32, within 1 ulp
   const float rm = __uint_as_float(__float_as_uint(r) - 1u), rp = __uint_as_float(__float_as_uint(r) + 1u);
@@ -161,11 +143,6 @@ __device__ __forceinline__ float sqrt_rn(float x) {
   r = (ep > 0.0f) ? rp : r;
   return r;
 }
-// diagnostic: parts of the fused eval skipped (1 formation error, 2 path length, 4 episode restart
-// writes, 8 the whole block; timing only, wrong metrics)
-#ifndef SWARM_EVAL_ABL
-#define SWARM_EVAL_ABL 0
-#endif
 
 // sqrt_rn's fast path alone, for branch-free loops: `tiny` records an input below 2^-96 (the
 // caller redoes the loop with sqrt_rn when any lane saw one; the value returned then is unused)
@@ -183,7 +160,6 @@ __device__ __forceinline__ double dsqrt_rn(double x) { return __builtin_sqrt(x);
 // products, rounded to float.  Returns the float sum s; the norm is sqrt_rn(s).
 __device__ __forceinline__ float sqsum_1d(float x, float y, float z) {
   const float xx = x * x, yy = y * y, zz = z * z;
-  if (SWARM_ABLATE & ABL_EXACT) return (xx + yy) + zz;
   return (float)(((double)xx + (double)yy) + (double)zz);
 }
 // np.linalg.norm(A, axis=1): float32 ((x*x)+(y*y))+(z*z).
@@ -199,17 +175,9 @@ __device__ __forceinline__ float sqsum_rank(float x, float y, float z) {
 // with ds_read_b96, banked (a/4) mod 32 in 8-lane groups, so two 16-B entries 128 B apart collide
 // (obstacle j and j + 8).  Keeping .w alive makes it one ds_read_b128, banked (a/4) mod 64 in
 // 16-lane groups: the 16-entry obstacle table is one bank row, conflict-free.
-#ifndef SWARM_LDS128
-#define SWARM_LDS128 1
-#endif
-#ifndef SWARM_S64_KEEPNB
-#define SWARM_S64_KEEPNB 1
-#endif
 __device__ __forceinline__ float4 lds_f4(const float4* __restrict__ p) {
   const float4 q = *p;
-#if SWARM_LDS128
   asm volatile("" ::"v"(q.w));
-#endif
   return q;
 }
 // Whole-wave rotate by one lane (DPP wave_ror:1, gfx9): lane i receives lane i-1's value.
@@ -408,9 +376,6 @@ __device__ __forceinline__ void pair_pass_wave(const float4* __restrict__ ring, 
 // that rotates one lane per rotation (DPP wave_ror:1, macc = ror(macc) + T_r for r = 31 .. 1,
 // then one more ror): the term of pair (t, t+r) lands on lane t+r.  1 VALU per pair instead of 2
 // on the receiving side.  Own terms are summed in f32 per group, then added in f64.
-#ifndef SWARM_PAIR_BATCH
-#define SWARM_PAIR_BATCH 4
-#endif
 template <int KS, int PASS, bool FAST, int RT, int NB, bool MIRROR>
 __device__ __forceinline__ void pair_group_w64(const float4* __restrict__ q0, uint32_t t4, float px, float py, float pz,
                                                bool self, uint32_t sflag, uint32_t keep, uint32_t keep_m, float ds,
@@ -464,7 +429,7 @@ __device__ __forceinline__ void pair_pass_w64(const float4* __restrict__ ring, i
   const uint32_t keep_m = keep & 0x7fffffffu;
   const uint32_t t4 = (uint32_t)t << 2;
   float macc = 0.f;
-  pair_groups_w64<KS, PASS, FAST, 31, SWARM_PAIR_BATCH>(ring + t, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk,
+  pair_groups_w64<KS, PASS, FAST, 31, S64_PAIR_BATCH>(ring + t, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk,
                                                         smin, fsum, macc);
   if constexpr (PASS == 1) fsum += (double)wave_ror1(macc);
   // rotation 32 pairs t with t+32 from both sides: own evaluation only
@@ -476,7 +441,10 @@ template <int KS, int PASS>
 __device__ __forceinline__ void pair_pass_block(const float4* __restrict__ pos4, int N, int t, float px, float py,
                                                 float pz, bool self, uint32_t keep, float ds,
                                                 uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum) {
-#pragma unroll 4
+  // runtime N: unrolled by 4 unless the body holds key inserts (their v_med3_u32 inline asm is
+  // convergent, which rules out the unroller's remainder loop)
+  constexpr int UNROLL = KS > 0 ? 1 : 4;
+#pragma unroll UNROLL
   for (int j = 0; j < N; ++j) {
     const float4 q = pos4[j];
     const float v = pair_value<PASS>(sqsum_f(q.x - px, q.y - py, q.z - pz));
@@ -522,7 +490,9 @@ __device__ __forceinline__ void pair_pass_block_fast(const float* __restrict__ p
   const float* q = pr + t * BLK_PAIR_STRIDE;
   float esum = 0.f;
   int r = 1;
-#pragma unroll 4
+  // runtime N: unrolled by 4 unless the body holds key inserts (convergent inline asm, above)
+  constexpr int UNROLL = KS > 0 && KEYS ? 1 : 4;
+#pragma unroll UNROLL
   for (; r + 1 < N; r += 2) {
     const float* e = q + r * BLK_PAIR_STRIDE;
     const blk_f2 X = {e[0], e[1]}, Y = {e[2], e[3]}, Z = {e[4], e[5]};
@@ -643,12 +613,6 @@ __device__ __forceinline__ float max_first(const float (&arr)[S], int K) {
 // K-th of the re-ranked survivors), so only points whose f32 squared sum lies within dmax^2 (plus
 // the f32 error band) can belong to the answer: a cheap scan filters, and the exact distance is
 // evaluated only for those few.
-#ifndef SWARM_FB_BATCH
-#define SWARM_FB_BATCH 8
-#endif
-#ifndef SWARM_FB_PRIO
-#define SWARM_FB_PRIO 0
-#endif
 template <int S, bool AXIS>
 __device__ __forceinline__ void exact_select(const float4* __restrict__ pts, int count, int self, int K, float dmax,
                                              float px, float py, float pz, float (&wd)[S], int (&wj)[S]) {
@@ -658,7 +622,7 @@ __device__ __forceinline__ void exact_select(const float4* __restrict__ pts, int
   // batches of 8 points: the batch's LDS reads are issued together and its filter sums computed
   // before the first (divergent) exact evaluation, instead of one exposed LDS round trip per
   // point — a wave in this fallback is the last of its launch more often than not
-  constexpr int B = SWARM_FB_BATCH;
+  constexpr int B = FB_BATCH;
 #pragma unroll 1
   for (int j0 = 0; j0 < count; j0 += B) {
     float4 q[B];
@@ -704,7 +668,7 @@ __device__ __forceinline__ bool exact_pair_collision(const float4* __restrict__ 
                                                      float px, float py, float pz, float s_thr) {
   bool c = false;
   const float s_cut = s_thr * FAST_HI;
-  constexpr int B = SWARM_FB_BATCH;  // batched LDS reads, as exact_select
+  constexpr int B = FB_BATCH;  // batched LDS reads, as exact_select
 #pragma unroll 1
   for (int j0 = 0; j0 < count; j0 += B) {
     float4 q[B];
@@ -720,24 +684,18 @@ __device__ __forceinline__ bool exact_pair_collision(const float4* __restrict__ 
   return c;
 }
 
-// step64 observation rows leave through write-through (sc1) buffer stores when SWARM_WT_STORES:
+// step64 observation rows leave through write-through (sc1) buffer stores when WT_STORES:
 // the lines are dropped from the XCD's L2 instead of staying dirty for the end-of-kernel
 // write-back (MI355X_MICROARCH.md, store flavours; a kernel boundary pays for the dirty bytes it
 // leaves): -5 % kernel time.  A compiler-visible buffer store (not inline asm) so the hazard and
 // waitcnt passes see it.  `base` must be wave-uniform (it becomes the buffer descriptor).
-#ifndef SWARM_WT_STORES
-#define SWARM_WT_STORES 1
-#endif
-#ifndef SWARM_OBS_STORE_AUX
-#define SWARM_OBS_STORE_AUX 16  // cache-policy bits of the obs buffer stores (16 = sc1)
-#endif
 constexpr int BUF_DWORD3 = 0x00020000;  // gfx9 raw buffer descriptor word 3
 __device__ __forceinline__ void store_obs(float* base, uint32_t nbytes, uint32_t byte_off, float4 v) {
-  if constexpr (SWARM_WT_STORES) {
+  if constexpr (WT_STORES) {
     typedef int v4i __attribute__((ext_vector_type(4)));
     const v4i d = {__float_as_int(v.x), __float_as_int(v.y), __float_as_int(v.z), __float_as_int(v.w)};
     __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)nbytes, BUF_DWORD3);
-    __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)byte_off, 0, SWARM_OBS_STORE_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)byte_off, 0, OBS_STORE_AUX);
   } else {
     *reinterpret_cast<float4*>(reinterpret_cast<char*>(base) + byte_off) = v;
   }
@@ -745,6 +703,8 @@ __device__ __forceinline__ void store_obs(float* base, uint32_t nbytes, uint32_t
 
 // ------------------------------------------------------------------ the kernel
 // LM (lane mode): 0 = BLOCK (L > 64), 1 = WAVE with 64/L teams, 2 = WAVE with one team (L == 64)
+}  // namespace swarm_dev
+namespace {  // kernels: internal to this translation unit
 template <int KIND, int DYN, int KS, int MSL, int LM>
 __global__ void __launch_bounds__(LM != 0 ? 64 : 1024)
 swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ actions,
@@ -754,9 +714,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   // compile-time mode in the step kernel; reset/observe share the aux kernel
   const int mode = (KIND == KIND_STEP) ? MODE_STEP : (mode_arg == MODE_RESET ? MODE_RESET : MODE_OBSERVE);
   STAMP(0);
-#ifdef SWARM_STAMPS
-  if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) g_stamps[blockIdx.x * 16 + 11] = __builtin_amdgcn_s_memrealtime();
-#endif
+  STAMP_BEGIN(blockIdx.x, threadIdx.x == 0);
   constexpr bool WAVE = LM != 0;
   constexpr bool W64 = LM == 2;
   const int tid = threadIdx.x;
@@ -975,11 +933,11 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   // block teams: the rotation pass over the pair-entry ring (N a power of two, kinematic)
   if constexpr (!WAVE && KS > 0 && DYN == DYN_KIN) fast = P.off_pair > 0 && __syncthreads_and(!is_agent || elig) != 0;
   const bool blk_rot = !WAVE && P.off_pair > 0;  // aux / reset passes of block teams rotate too
-  if (pass_env && !(SWARM_ABLATE & ABL_PAIR)) {
+  if (pass_env) {
     if (mode == MODE_STEP) {
       constexpr int PASS = (DYN == DYN_KIN) ? 1 : 2;
       if constexpr (WAVE) {
-        if constexpr (W64 && !(SWARM_ABLATE & ABL_W64)) {
+        if constexpr (W64) {
           if (fast) pair_pass_w64<KS, PASS, true>(ring, t, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
           else pair_pass_w64<KS, PASS, false>(ring, t, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
         } else {
@@ -996,12 +954,11 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
           pair_pass_block<KS, PASS>(ring, N, t, px, py, pz, elig, P.nb_keep, P.ds_f, nk, smin, fsum);
         }
       }
-      if constexpr (SWARM_ABLATE & ABL_OBST) {}
-      else if constexpr (DYN == DYN_KIN) obstacle_pass<MSL, true>(obst4, Me, px, py, pz, act, C.s_obst, P.ob_keep, ok, ocoll);
+      if constexpr (DYN == DYN_KIN) obstacle_pass<MSL, true>(obst4, Me, px, py, pz, act, C.s_obst, P.ob_keep, ok, ocoll);
       else obstacle_pass<MSL, true>(obst4, Me, px, py, pz, true, C.s_phys_obst, P.ob_keep, ok, ocoll);
     } else {
       if constexpr (WAVE) {
-        if constexpr (W64 && !(SWARM_ABLATE & ABL_W64)) pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
+        if constexpr (W64) pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
         else pair_pass_wave<KS, 0, true>(ring, L, t, tid, px, py, pz, true, P.nb_keep, 0.f, nk, smin, fsum);
       } else {
         if (blk_rot) pair_pass_block_fast<KS, 0>(pair_ring, N, t, px, py, pz, P.nb_keep, 0.f, nk, fsum, smin);
@@ -1025,7 +982,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
   auto select_topk = [&](bool run, bool dkey, bool rot) {
     const int Mse = Ms < Me ? Ms : Me;
     bool slow_nb = false, slow_ob = false;
-    if (run && !(SWARM_ABLATE & ABL_FINISH)) {
+    if (run) {
       const int imod = rot ? (L - 1) : 0x7fffffff;
       if constexpr (KS > 0) slow_nb = !finish_keys<KS, false, true>(nk, ring, N, rot ? t : 0, imod, Kq, P.nb_keep, dkey, px, py, pz, wd, wj);
       if constexpr (MSL > 0) slow_ob = !finish_keys<MSL, true, false>(ok, obst4, Me, 0, 0x7fffffff, Mse, P.ob_keep, false, px, py, pz, od, oj);
@@ -1139,7 +1096,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
       trunc = trunc_all;
       cont = true;
     }
-    do_reset = P.auto_reset && env_ok && (term_all || trunc_all) && !(SWARM_ABLATE & ABL_RESET);
+    do_reset = P.auto_reset && env_ok && (term_all || trunc_all);
     bool dkey_step = DYN == DYN_KIN;
     if constexpr (!WAVE && DYN == DYN_KIN) {
       if (fast && !do_reset) {  // block uniform: the keys of the emitted observation
@@ -1188,7 +1145,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
         float s2 = 0.f;
         double f2 = 0.0;
         if constexpr (WAVE) {
-          if constexpr (W64 && !(SWARM_ABLATE & ABL_W64)) pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
+          if constexpr (W64) pair_pass_w64<KS, 0, true>(ring, t, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
           else pair_pass_wave<KS, 0, true>(ring, L, t, tid, px, py, pz, true, P.nb_keep, 0.f, nk, s2, f2);
         } else if (blk_rot) {
           pair_pass_block_fast<KS, 0>(pair_ring, N, t, px, py, pz, P.nb_keep, 0.f, nk, f2, s2);
@@ -1314,8 +1271,7 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     }
   };
 
-  if (SWARM_ABLATE & ABL_OBS) {
-  } else if ((mode != MODE_STEP && env_mask != nullptr) || (LM != 2 && P.obs_direct)) {
+  if ((mode != MODE_STEP && env_mask != nullptr) || (LM != 2 && P.obs_direct)) {
     // masked reset/observe (off the hot path), and small multi-team launches (latency-bound: the
     // LDS round trip and barriers of the staging lengthen every wave): rows straight to memory
     if (is_agent && sel) write_row(O.obs + (size_t)ag * D);
@@ -1354,14 +1310,10 @@ swarm_kernel(const KParams P, const swarm_state_t S, const float* __restrict__ a
     }
   }
   STAMP(8);
-#ifdef SWARM_STAMPS
-  if (threadIdx.x == 0 && blockIdx.x < (1 << 16)) {
-    g_stamps[blockIdx.x * 16 + 9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
-    g_stamps[blockIdx.x * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-    g_stamps[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
+  STAMP_END(blockIdx.x, threadIdx.x == 0);
 }
+}  // namespace
+namespace swarm_dev {
 
 // ------------------------------------------------------------------ step64: the headline kernel
 // Specialisation of the step for one env of exactly 64 drones per 64-lane wave, kinematic
@@ -1386,21 +1338,15 @@ constexpr int S64_RING = 96;
 // aliases the wave's ring and obstacles (dead once the rows are built in registers), so 32-row
 // chunks (4.6 KB per wave, 148 KB for 32 waves per CU) fit: half the chunk passes and LDS row
 // writes of 16-row chunks.
-#ifndef SWARM_S64_CH
-#define SWARM_S64_CH 32
-#endif
-constexpr int S64_CH = SWARM_S64_CH;
+[[maybe_unused]] constexpr int S64_CH = S64_CH_ROWS;
 constexpr int S64_HEADS = 8;  // env-queue heads, one per XCD (blockIdx mod 8)
 constexpr int S64_HEAD_STRIDE = SWARM_WORK_WORDS / S64_HEADS;  // one 128-B line per head
-constexpr int S64_WPS_DEFAULT = 0;  // persistent grid only on request (waves_per_simd > 0): slower here
+[[maybe_unused]] constexpr int S64_WPS_DEFAULT = 0;  // persistent grid only on request (waves_per_simd > 0): slower here
 constexpr int S64_MIN_WAVES = 6;    // register budget of swarm_step64 (<= 80 VGPRs)
 
 // LDS ordering inside one wave: every LDS region of the step64 body belongs to one wave, whose
 // LDS instructions execute in issue order, so a compiler fence is all that is needed (several
 // envs share a workgroup without coupling their waves through s_barrier).
-#ifndef SWARM_PRIO_MODE
-#define SWARM_PRIO_MODE 0
-#endif
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1551,7 +1497,7 @@ __device__ __forceinline__ void pair_pass_s64(const float* __restrict__ soa, int
   asm volatile("" : "+v"(s0));
   float macc = 0.f;
   // every caller starts the pass with an empty key list (F0 = 0)
-  pair_groups_s64<KS, PASS, FAST, 31, SWARM_PAIR_BATCH, 0>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk,
+  pair_groups_s64<KS, PASS, FAST, 31, S64_PAIR_BATCH, 0>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk,
                                                            smin, fsum, macc);
   if constexpr (PASS == 1) fsum += (double)wave_ror1(macc);
   // rotation 32 pairs t with t+32 from both sides: own evaluation only
@@ -1848,13 +1794,9 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   const size_t ea = (size_t)env * S64_N;  // first agent of the env (uniform)
   float* __restrict__ const soa = reinterpret_cast<float*>(ring + S64_N);  // S64Lds::w.soa
   S64ArgPtr A = s64_args();  // re-fetched at every phase boundary
-#ifdef SWARM_STAMPS
-  const int srec = env + (int)A->P.env_offset;  // stamp record: the global env (env groups)
-#endif
+  STAMP_VAR(const int srec = env + (int)A->P.env_offset);  // stamp record: the global env (env groups)
   STAMP_AT(srec, 0);
-#ifdef SWARM_STAMPS
-  if ((threadIdx.x & 63) == 0 && srec < (1 << 16)) g_stamps[srec * 16 + 11] = __builtin_amdgcn_s_memrealtime();
-#endif
+  STAMP_BEGIN(srec, (threadIdx.x & 63) == 0);
 
   // ---- inputs (prefetched): env-uniform scalars, per-lane rows, obstacles to LDS
   float gx = __uint_as_float(__builtin_amdgcn_readlane(c.gse, 0));
@@ -1944,7 +1886,6 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   s64_put(ring, soa, t, px, py, pz, (DYN == DYN_PHYS || act) ? 1.f : 0.f);
   wave_sync();
   prefetch();  // `c` is dead from here on
-  if constexpr (SWARM_PRIO_MODE >= 2) __builtin_amdgcn_s_setprio(1);
   STAMP_AT(srec, 2);
   A = s64_args();
 
@@ -1959,27 +1900,6 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   double fsum = 0.0;
   const bool fast = DYN == DYN_PHYS || __all(act);
   bool early = false;  // kinematic: the episode ends whatever the pair pass finds (no keys needed)
-#if SWARM_DIAG_EXTRA_VALU
-  {  // diagnostic: SWARM_DIAG_EXTRA_VALU dependent-free FAST VALU ops per wave
-    float z0 = px, z1 = py, z2 = pz, z3 = px + 1.f;
-#pragma unroll
-    for (int i = 0; i < SWARM_DIAG_EXTRA_VALU / 4; ++i) {
-      z0 = z0 * 0.999f; z1 = z1 * 0.999f; z2 = z2 * 0.999f; z3 = z3 * 0.999f;
-    }
-    if (z0 + z1 + z2 + z3 == 1234.5f) fsum += 1.0;
-  }
-#endif
-#if SWARM_DIAG_EXTRA_INT
-  {  // diagnostic: SWARM_DIAG_EXTRA_INT dependent-free v_min_u32 / v_max_u32 per wave (the key-insert class)
-    uint32_t z0 = __float_as_uint(px), z1 = __float_as_uint(py), z2 = __float_as_uint(pz), z3 = (uint32_t)t;
-#pragma unroll
-    for (int i = 0; i < SWARM_DIAG_EXTRA_INT / 4; ++i) {
-      z0 = min(z0, z1); z1 = max(z1, z2); z2 = min(z2, z3); z3 = max(z3, z0);
-      asm volatile("" : "+v"(z0), "+v"(z1), "+v"(z2), "+v"(z3));
-    }
-    if (z0 + z1 + z2 + z3 == 12345u) fsum += 1.0;
-  }
-#endif
   if constexpr (DYN == DYN_PHYS) {  // s' keys, no formation; every drone is a contact candidate
     pair_pass_s64<KS, 2, true>(soa, t, px, py, pz, true, A->P.nb_keep, 0.f, nk, smin, fsum);
     obstacle_pass_s64<MSL, true>(osoa, M, px, py, pz, true, A->P.s_phys_obst, A->P.ob_keep, ok, ocoll);
@@ -1988,26 +1908,16 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     // the pair pass finds, so such an env — ~half of the resetting ones — runs the pair pass
     // without neighbour keys (they would rank the positions the reset replaces): formation terms
     // and the running minimum only, the same sums bit for bit
-    if (SWARM_ABLATE & ABL_OBST) {  // diagnostic: obstacle collisions only, no obstacle keys
-      uint32_t ok0[1];
-      obstacle_pass_s64<0, true>(osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok0, ocoll);
-    } else {
-      obstacle_pass_s64<MSL, true>(osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
-    }
+    obstacle_pass_s64<MSL, true>(osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
     A = s64_args();
-    early = fast && A->P.auto_reset && !(SWARM_ABLATE & ABL_RESET) &&
+    early = fast && A->P.auto_reset &&
             (__ballot(act && ocoll) != 0 || stepc + 1 >= A->P.max_steps);
-#if SWARM_DIAG_NO_FORMATION
-    if (fast) pair_pass_s64<KS, 0, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
-#else
     if (early) {
       uint32_t nk0[1] = {KEY_EMPTY};
       pair_pass_s64<0, 1, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk0, smin, fsum);
     } else if (fast) {
       pair_pass_s64<KS, 1, true>(soa, t, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
-    }
-#endif
-    else pair_pass_s64<KS, 1, false>(soa, t, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
+    } else pair_pass_s64<KS, 1, false>(soa, t, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, fsum);
   }
   if constexpr (LANDED) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next env's inputs are in
   STAMP_AT(srec, 3);
@@ -2016,7 +1926,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   // ---- exact top-K (finish_keys, rare exact_select)
   float wd[KS], od[MSL];
   int wj[KS], oj[MSL];
-  // the obs row's neighbour columns p_j - p (SWARM_S64_KEEPNB): the finish's own differences, kept
+  // the obs row's neighbour columns p_j - p: the finish's own differences, kept
   // in registers to the row build instead of a second random ring gather (LDS bank conflicts)
   float nd[3 * S64_K];
   auto regather_nd = [&]() {
@@ -2027,47 +1937,16 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     }
   };
   auto select_topk = [&](bool dkey) {
-    if (SWARM_ABLATE & ABL_FINISH) {  // diagnostic: the keys as the answer (wrong distances)
-#pragma unroll
-      for (int s = 0; s < KS; ++s) { wd[s] = __uint_as_float(nk[s] & A->P.nb_keep); wj[s] = (int)(nk[s] & 63u) + t; }
-#pragma unroll
-      for (int s = 0; s < MSL; ++s) { od[s] = __uint_as_float(ok[s] & A->P.ob_keep); oj[s] = (int)(ok[s] & 15u); }
-      regather_nd();
-      return;
-    }
     const uint32_t fflags = s64_finish_fast<KS, MSL>(nk, ok, ring, obst, t, M, A->P.nb_keep, A->P.ob_keep, dkey, px, py,
                                                      pz, wd, wj, od, oj, nd);
     const uint64_t fails = __ballot(fflags != 0);
-#ifdef SWARM_DIAG_FINISH  // diagnostic counters (stamps build): waves / lanes through the general finish
-    if (t == 0) {
-      atomicAdd(&g_stamps[(1 << 19) + 0], 1ull);
-      if (fails) { atomicAdd(&g_stamps[(1 << 19) + 1], 1ull); atomicAdd(&g_stamps[(1 << 19) + 2], (unsigned long long)__popcll(fails)); }
-    }
-#endif
-    if (SWARM_ABLATE & ABL_GENKEEP) {  // diagnostic: keep the checks alive, never take the general path
-      if (fails == 0x123456789abcdefull) wd[0] = 0.f;
-      return;
-    }
-    if (fails == 0 || (SWARM_ABLATE & ABL_GENERAL)) return;
-    if constexpr (SWARM_FB_PRIO > 0) __builtin_amdgcn_s_setprio(SWARM_FB_PRIO);  // a fallback wave is its launch's last
+    if (fails == 0) return;
     bool slow_nb, slow_ob;
     s64_finish_general<KS, MSL>(fflags, nk, ok, ring, obst, t, M, A->P.nb_keep, A->P.ob_keep, dkey, px, py, pz, wd, wj,
                                 od, oj, slow_nb, slow_ob);
-#ifdef SWARM_DIAG_FINISH
-    {
-      const uint64_t bn = __ballot(slow_nb), bo = __ballot(slow_ob);
-      if (t == 0) {
-        if (bn) { atomicAdd(&g_stamps[(1 << 19) + 3], 1ull); atomicAdd(&g_stamps[(1 << 19) + 4], (unsigned long long)__popcll(bn)); }
-        if (bo) { atomicAdd(&g_stamps[(1 << 19) + 5], 1ull); atomicAdd(&g_stamps[(1 << 19) + 6], (unsigned long long)__popcll(bo)); }
-        if (!dkey) atomicAdd(&g_stamps[(1 << 19) + 7], 1ull);
-      }
-    }
-#endif
-    if (!(SWARM_ABLATE & ABL_EXSEL)) {
-      if (slow_nb) exact_select<KS, false>(ring, S64_N, t, S64_K, max_first(wd, S64_K), px, py, pz, wd, wj);
-      if (slow_ob) exact_select<MSL, true>(obst, M, -1, S64_MS, max_first(od, S64_MS), px, py, pz, od, oj);
-    }
-    if (SWARM_S64_KEEPNB) regather_nd();  // the general finish may have re-ranked the neighbours
+    if (slow_nb) exact_select<KS, false>(ring, S64_N, t, S64_K, max_first(wd, S64_K), px, py, pz, wd, wj);
+    if (slow_ob) exact_select<MSL, true>(obst, M, -1, S64_MS, max_first(od, S64_MS), px, py, pz, od, oj);
+    regather_nd();  // the general finish may have re-ranked the neighbours
   };
   STAMP_AT(srec, 4);
 
@@ -2152,7 +2031,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       }
     }
   }
-  const bool do_reset = A->P.auto_reset && (term_all || trunc_all) && !(SWARM_ABLATE & ABL_RESET);
+  const bool do_reset = A->P.auto_reset && (term_all || trunc_all);
   (A->O.reward + ea)[t] = rew;
   if (A->O.dist_goal) (A->O.dist_goal + ea)[t] = curr;
   if (A->O.info_flags)
@@ -2165,7 +2044,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   const uint64_t m_term = __ballot(term), m_trunc = __ballot(trunc);
   bool ev_restart = false;  // fused eval: a live episode ended here and the env restarts
   if constexpr (EVAL) __builtin_amdgcn_sched_barrier(0);  // the finish's reads stay below the eval block
-  if (EVAL && DYN == DYN_KIN && !(SWARM_EVAL_ABL & 8) && A->EV.status != nullptr) {
+  if (EVAL && DYN == DYN_KIN && A->EV.status != nullptr) {
     // fused eval (out.eval, SWARM_EVAL_STEP_FUSED): everything swarm_eval_update does for one step
     // (swarm_eval.hip eval_update_kernel: the same arithmetic, the same f64 butterflies), with the
     // positions already in registers / LDS: episode reward += mean reward of the stepped agents,
@@ -2177,7 +2056,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       const bool not_reached = __ballot(cont && !reached) != 0;
       const uint64_t m_obs = __ballot(cont);
       const int n_obs = __popcll(m_obs);
-      if (cont && !(SWARM_EVAL_ABL & 2)) {
+      if (cont) {
         // path length += |last - p| (evaluate_protocol.py's _distance: the sdot-double norm); last =
         // the position this step started from, still in the state (written back below): an agent
         // observed now was observed at the previous step or stands at its episode's start
@@ -2192,7 +2071,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
       // sums end uniform and are moved to SGPRs at once (short VGPR live ranges: the kernel runs
       // at 64 VGPRs)
       double fe = 0.0;
-      if (n_obs > 1 && !(SWARM_EVAL_ABL & 1)) {
+      if (n_obs > 1) {
         const double sp = A->EV.spacing;
         const bool all = n_obs == S64_N;
         // one pass: the square roots without sqrt_rn's per-call slow-path branch (a branch per
@@ -2316,20 +2195,13 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   // ---- in-kernel auto-reset (wave-uniform): new episode, then its key passes
   uint32_t episode_new = episode0;
   if (do_reset) {
-    if constexpr (SWARM_PRIO_MODE >= 1) __builtin_amdgcn_s_setprio(3);  // longest remaining work first
     const long long genv = A->P.env_offset + env;
     episode_new = episode0 + 1u;
     // two independent Philox chains per lane: drone t (block t), and obstacle t (block N + t) for
     // lanes t < M / the goal (block N + M) on lane M
     uint32_t w[4], wo[4];
-    if (SWARM_ABLATE & ABL_PHILOX) {  // diagnostic: cheap stand-in draws (wrong values)
-      const uint32_t h0 = ((uint32_t)t + episode_new * 0x9E3779B9u) * 0x85EBCA6Bu ^ (uint32_t)genv;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) { w[k] = h0 * (2u * k + 1u); wo[k] = (h0 ^ 0x55u) * (2u * k + 3u); }
-    } else {
-      draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)t, w);
-      draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)(S64_N + (t < M ? t : M)), wo);
-    }
+    draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)t, w);
+    draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)(S64_N + (t < M ? t : M)), wo);
     const float lo_w = A->P.neg_half_w, wd_w = A->P.width_w;
     px = uni(w[0], lo_w, wd_w);
     py = uni(w[1], lo_w, wd_w);
@@ -2351,21 +2223,19 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     gz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(goal_z), M));
     s64_put(ring, soa, t, px, py, pz, 1.f);
     wave_sync();
-    if (!(SWARM_ABLATE & ABL_RESET_WORK)) {
 #pragma unroll
-      for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
+    for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
 #pragma unroll
-      for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
-      bool c2 = false;
-      float s2 = 0.f;
-      double f2 = 0.0;
-      pair_pass_s64<KS, 0, true>(soa, t, px, py, pz, true, A->P.nb_keep, 0.f, nk, s2, f2);
-      if (!(SWARM_ABLATE & ABL_OBST)) obstacle_pass_s64<MSL, false>(osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
-    }
+    for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
+    bool c2 = false;
+    float s2 = 0.f;
+    double f2 = 0.0;
+    pair_pass_s64<KS, 0, true>(soa, t, px, py, pz, true, A->P.nb_keep, 0.f, nk, s2, f2);
+    obstacle_pass_s64<MSL, false>(osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
   }
   // one call site for both (the new episode's s' keys, the kinematic step pass's d~ keys; physics
   // ranks by s'): the finish and its general fallback are emitted once, not once per branch
-  if (!(do_reset && (SWARM_ABLATE & ABL_RESET_WORK))) select_topk(DYN == DYN_KIN && !do_reset);
+  select_topk(DYN == DYN_KIN && !do_reset);
 
   STAMP_AT(srec, 6);
   A = s64_args();
@@ -2413,7 +2283,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     gs[3 * S64_N + t3] = vx; gs[3 * S64_N + t3 + 1] = vy; gs[3 * S64_N + t3 + 2] = vz;
     if (t == 0) { gs[6 * S64_N + 0] = gx; gs[6 * S64_N + 1] = gy; gs[6 * S64_N + 2] = gz; }
   }
-  if (EVAL && DYN == DYN_KIN && ev_restart && !(SWARM_EVAL_ABL & 4)) {
+  if (EVAL && DYN == DYN_KIN && ev_restart) {
     // fused eval: the next episode opens from its first observation (eval_update_kernel's
     // restart: start = p, goal = p + obs[6:9] = p + (g - p), path length 0)
     float* st0 = A->EV.start + (ea + t) * 3;
@@ -2441,56 +2311,15 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
 #pragma unroll
   for (int s = 0; s < S64_K; ++s) {
-    if (SWARM_S64_KEEPNB) {
-      row[9 + 4 * s] = nd[3 * s]; row[10 + 4 * s] = nd[3 * s + 1]; row[11 + 4 * s] = nd[3 * s + 2];
-    } else {
-      const float4 q = (SWARM_ABLATE & ABL_ROWGATHER) ? make_float4((float)wj[s], 0.f, 0.f, 0.f)
-                                                      : s64_ring_gather(ring, wj[s] & (S64_N - 1), px, py, pz);
-      row[9 + 4 * s] = q.x - px; row[10 + 4 * s] = q.y - py; row[11 + 4 * s] = q.z - pz;
-    }
+    row[9 + 4 * s] = nd[3 * s]; row[10 + 4 * s] = nd[3 * s + 1]; row[11 + 4 * s] = nd[3 * s + 2];
     row[12 + 4 * s] = wd[s];
   }
 #pragma unroll
   for (int s = 0; s < S64_MS; ++s) {
-    const float4 q = (SWARM_ABLATE & ABL_ROWGATHER) ? make_float4((float)oj[s], 0.f, 0.f, 0.f) : lds_f4(obst + (oj[s] & (S64_MMAX - 1)));
+    const float4 q = lds_f4(obst + (oj[s] & (S64_MMAX - 1)));
     row[21 + 4 * s] = q.x - px; row[22 + 4 * s] = q.y - py; row[23 + 4 * s] = q.z - pz; row[24 + 4 * s] = od[s];
   }
-  if (SWARM_ABLATE & ABL_OBS) return;
   constexpr int V4 = CH * D / 4;  // float4 per chunk
-  float4* __restrict__ dst = reinterpret_cast<float4*>(A->O.obs + ea * D);
-  if (SWARM_ABLATE & ABL_STORE_ONLY) {  // diagnostic: the obs stores without the LDS staging (wrong values)
-#pragma unroll
-    for (int ch = 0; ch < S64_N / CH; ++ch)
-#pragma unroll
-      for (int i = t; i < V4; i += 64) dst[ch * V4 + i] = make_float4(row[i & 7], row[9 + (i & 7)], row[18], row[30]);
-    return;
-  }
-  if (SWARM_ABLATE & ABL_ROW_ONLY) {  // diagnostic: the obs row computed, neither staged nor stored
-    float acc = 0.f;
-#pragma unroll
-    for (int i = 0; i < D; ++i) acc += row[i];
-    if (acc == 12345.f) dst[t] = make_float4(acc, acc, acc, acc);
-    return;
-  }
-  if (SWARM_ABLATE & ABL_STAGE_ONLY) {  // diagnostic: the LDS staging without the obs stores
-    float acc = 0.f;
-    wave_sync();
-    float* srow0 = stage + (t % CH) * D;
-#pragma unroll
-    for (int ch = 0; ch < S64_N / CH; ++ch) {
-      if (t / CH == ch) {
-#pragma unroll
-        for (int i = 0; i < D; ++i) srow0[i] = row[i];
-      }
-      wave_sync();
-      const float4* s4 = reinterpret_cast<const float4*>(stage);
-#pragma unroll
-      for (int i = t; i < V4; i += 64) { const float4 q = s4[i]; acc += q.x + q.y + q.z + q.w; }
-      wave_sync();
-    }
-    if (acc == 12345.f) dst[t] = make_float4(acc, acc, acc, acc);
-    return;
-  }
   wave_sync();  // the stage aliases ring / obstacles: every row-build read is issued before it
   const float4* s4 = reinterpret_cast<const float4*>(stage);
   float* srow = stage + (t % CH) * D;
@@ -2520,13 +2349,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     wave_sync();
   }
   STAMP_AT(srec, 8);
-#ifdef SWARM_STAMPS
-  if ((threadIdx.x & 63) == 0 && srec < (1 << 16)) {
-    g_stamps[srec * 16 + 9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
-    g_stamps[srec * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-    g_stamps[srec * 16 + 12] = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
+  STAMP_END(srec, (threadIdx.x & 63) == 0);
 }
 
 // The kernel.  Without a work buffer (S.work == NULL): one env per workgroup.  With one: a
@@ -2541,48 +2364,15 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
 // Software pipeline: once env i has consumed its inputs (after integrate), the inputs of env i+1
 // and the ticket of env i+2 are issued; they land while env i finishes, and env i's stores
 // drain while env i+1 computes.
-// Diagnostic: wave priority cohorts (s_setprio by blockIdx) to stagger when waves finish.
-#ifndef SWARM_PRIO_LEVELS
-#define SWARM_PRIO_LEVELS 0
-#endif
-#ifndef SWARM_PRIO_MODE
-#define SWARM_PRIO_MODE 0
-#endif
-#ifndef SWARM_GROUP_PRIO
-#define SWARM_GROUP_PRIO 0
-#endif
-__device__ __forceinline__ void s64_set_priority() {
-  if constexpr (SWARM_GROUP_PRIO > 0) {
-    // diagnostic: env groups alternate priority (group g starts at env_offset = g * E_g), so the
-    // two groups' compute phases do not share the SIMDs' issue evenly
-    S64ArgPtr A = s64_args();
-    const long long q = A->P.E > 0 ? A->P.env_offset / A->P.E : 0;
-    if ((q & 1) == 0) __builtin_amdgcn_s_setprio(SWARM_GROUP_PRIO);
-  }
-  if constexpr (SWARM_PRIO_LEVELS > 1) {
-    const int lvl = (int)((blockIdx.x >> 3) % SWARM_PRIO_LEVELS) * 3 / (SWARM_PRIO_LEVELS - 1);
-    switch (lvl) {
-      case 0: __builtin_amdgcn_s_setprio(3); break;
-      case 1: __builtin_amdgcn_s_setprio(2); break;
-      case 2: __builtin_amdgcn_s_setprio(1); break;
-      default: __builtin_amdgcn_s_setprio(0); break;
-    }
-  }
-}
 
 // One wave per env (the launch when the grid covers E): no loop, 8 waves per SIMD.  G envs per
 // workgroup of G independent waves: 8192 one-wave workgroups take the dispatcher ~4 us to start,
 // a quarter as many 4-wave ones about 1 us.
-#ifndef SWARM_S64_WG_ENVS
-#define SWARM_S64_WG_ENVS 4
-#endif
-constexpr int S64_WG_ENVS = SWARM_S64_WG_ENVS;
+[[maybe_unused]] constexpr int S64_WG_ENVS = S64_WG_ENVS_C;
 // The body of both one-wave-per-env kernels (kinematic / physics).
 template <int CH, int G, int DYN, bool EVAL = false>
 __device__ __forceinline__ void s64_once_body() {
   __shared__ S64Lds<CH> lds[G];
-  s64_set_priority();
-  if constexpr (SWARM_PRIO_MODE >= 2) __builtin_amdgcn_s_setprio(3);  // inputs and integrate first
   const int t = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int env = blockIdx.x * G + w;
@@ -2592,23 +2382,26 @@ __device__ __forceinline__ void s64_once_body() {
   s64_env<CH, false, void (*)(), DYN, EVAL>(env, s64_args()->P.M, cur, lds[w].w.ring, lds[w].w.obst,
                                       reinterpret_cast<float*>(lds[w].stage), t, []() {});
 }
+}  // namespace swarm_dev
+namespace {  // kernels: internal to this translation unit
 template <int CH, int G>
 __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(8)))
 swarm_step64_once(const S64Args args) {
   (void)args;  // read through s64_args()
   s64_once_body<CH, G, DYN_KIN>();
 }
+}  // namespace
+namespace swarm_dev {
 // The physics restatement (DronePhysicsEnv, point mass) at the same shape: the
 // same rings, passes, finish and obs staging, with the substep integrate, s' keys, contact
 // thresholds, physics rewards / terminations, reset ranges and the clamped obs velocity of
 // swarm_kernel<0, DYN_PHYS, 4, 5, 2>, bit for bit.
 // The headline step with the evaluation protocol fused in (out.eval, SWARM_EVAL_STEP_FUSED):
 // a separate instantiation, so the plain step's registers and schedule are untouched.
-#ifndef SWARM_S64_EVAL_WAVES
-#define SWARM_S64_EVAL_WAVES 8
-#endif
+}  // namespace swarm_dev
+namespace {  // kernels: internal to this translation unit
 template <int CH, int G>
-__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(SWARM_S64_EVAL_WAVES)))
+__global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(S64_EVAL_WAVES)))
 swarm_step64_eval_once(const S64Args args) {
   (void)args;
   s64_once_body<CH, G, DYN_KIN, true>();
@@ -2619,7 +2412,11 @@ swarm_step64_phys_once(const S64Args args) {
   (void)args;
   s64_once_body<CH, G, DYN_PHYS>();
 }
+}  // namespace
+namespace swarm_dev {
 
+}  // namespace swarm_dev
+namespace {  // kernels: internal to this translation unit
 template <int CH>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(S64_MIN_WAVES)))
 swarm_step64(const S64Args args) {
@@ -2654,15 +2451,7 @@ swarm_step64(const S64Args args) {
     if (head != nullptr && t == 0) v = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return v;
   };
-#ifdef SWARM_S64_STATIC  // diagnostic: static stride assignment instead of the env queues
-  head = nullptr;
-  env = blockIdx.x;
-#endif
   auto settle = [&](uint32_t v) -> int {
-#ifdef SWARM_S64_STATIC
-    (void)v;
-    return env + (int)gridDim.x < A->P.E ? env + (int)gridDim.x : -1;
-#endif
     if (head == nullptr) return -1;
     v = __builtin_amdgcn_readfirstlane(v);
     if (v == n_draws - 1u && t == 0) __hip_atomic_store(head, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2688,6 +2477,8 @@ swarm_step64(const S64Args args) {
   }
   if (!first) settle(ticket);
 }
+}  // namespace
+namespace swarm_dev {
 
 // ------------------------------------------------------------------ step16q: config 2 (N = 16)
 // BASELINE config 2 (N = 16 drones x E = 1024 envs) is a latency-bound launch: 1,024 envs of
@@ -2712,8 +2503,7 @@ constexpr int Q_K = 3;
 constexpr int Q_MS = 4;
 constexpr int Q_D = 9 + 4 * Q_K + 4 * Q_MS;  // 37
 constexpr int Q_MMAX = 16;
-constexpr uint64_t Q_LEAD = 0x1111111111111111ull;  // quarter 0 of every drone
-constexpr int Q_WG_ENVS = 4;                        // independent one-env waves per workgroup
+[[maybe_unused]] constexpr uint64_t Q_LEAD = 0x1111111111111111ull;  // quarter 0 of every drone
 
 union Q16Lds {
   struct {
@@ -2727,6 +2517,7 @@ union Q16Lds {
   float4 stage[Q_N * Q_D / 4];
 };
 
+#if SWARM_HAS_PART(6)  // step16q's device code: its own translation unit
 // DPP quad permutations: xor 1, xor 2, broadcast of quad lane k
 __device__ __forceinline__ uint32_t quad_xor1(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false); }
 __device__ __forceinline__ uint32_t quad_xor2(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false); }
@@ -3014,58 +2805,35 @@ __device__ __forceinline__ void q16_next_episode(S64ArgPtr A, int env, int lane,
   q16_store_obs(A, H, ea, lane);
 }
 
-#ifdef SWARM_STAMPS
-#define Q16_FLAG(f) (q16_flags |= (f))  // slow paths a wave took (tools/stamps16.py)
-#else
-#define Q16_FLAG(f) ((void)0)
-#endif
 // step16q (one wave per SIMD, latency-bound) reads the kernarg segment through one pointer, so
 // the compiler batches the parameter loads at the top instead of a dependent scalar round trip at
 // each phase: 6.85 -> 6.80 us (step256 measured 46.8 -> 47.5-48.2 us that way and keeps step64's
-// per-phase re-fetch; SWARM_LAT_REFETCH_ON=1 restores it here, diagnostics only).
-#ifndef SWARM_LAT_REFETCH_ON
-#define SWARM_LAT_REFETCH_ON 0
-#endif
-#ifndef SWARM_Q16_FLOOR
-#define SWARM_Q16_FLOOR 0
-#endif
-#define SWARM_LAT_REFETCH(A) \
-  do {                       \
-    if (SWARM_LAT_REFETCH_ON) (A) = s64_args(); \
-  } while (0)
+// per-phase re-fetch).
 // 71 VGPRs without spills at 4 waves per EU (at 8: 64 VGPRs and 4 spilled, scratch round trips
 // on a latency-bound launch): config 2 (one wave per SIMD) 6.58 vs 6.85 us per step
-#ifndef SWARM_Q16_WAVES_PER_EU
-#define SWARM_Q16_WAVES_PER_EU 4
-#endif
-// SPEC: one env per 2-wave workgroup, wave 1 running q16_next_episode (G must be 1)
-template <int G, bool SPEC = false>
-__global__ void __launch_bounds__(SPEC ? 128 : 64 * G) __attribute__((amdgpu_waves_per_eu(SWARM_Q16_WAVES_PER_EU)))
+// One env per 2-wave workgroup: wave 0 steps the env, wave 1 runs q16_next_episode.
+}  // namespace swarm_dev
+namespace {  // kernels: internal to this translation unit
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(Q16_WAVES_PER_EU)))
 swarm_step16q(const S64Args args) {
   (void)args;  // read through s64_args()
-  static_assert(!SPEC || G == 1, "the 2-wave launch holds one env per workgroup");
   constexpr int KS = Q_K + 1, MSL = Q_MS + 1;
-  __shared__ Q16Lds ldsq[SPEC ? 2 : G];
-  __shared__ uint32_t decision;  // SPEC: wave 0's reset decision for wave 1
+  __shared__ Q16Lds ldsq[2];
+  __shared__ uint32_t decision;  // wave 0's reset decision for wave 1
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int w = SPEC ? 0 : wv;
   S64ArgPtr A = s64_args();
-  const int env = blockIdx.x * G + w;
-  if (env >= A->P.E) return;  // whole wave (workgroup)
-  if constexpr (SPEC) {
-    if (wv == 1) {
-      if (A->P.auto_reset) q16_next_episode(A, env, lane, ldsq[1], &decision);
-      return;
-    }
+  const int env = blockIdx.x;
+  if (env >= A->P.E) return;  // whole workgroup
+  if (wv == 1) {
+    if (A->P.auto_reset) q16_next_episode(A, env, lane, ldsq[1], &decision);
+    return;
   }
-  Q16Lds& L = ldsq[w];
+  Q16Lds& L = ldsq[0];
   const int d = lane >> 2, q = lane & 3;
   STAMP_AT(env, 0);
-#ifdef SWARM_STAMPS
-  if (lane == 0 && env < (1 << 16)) g_stamps[env * 16 + 11] = __builtin_amdgcn_s_memrealtime();
-  uint32_t q16_flags = 0u;
-#endif
+  STAMP_BEGIN(env, lane == 0);
+  Q16_FLAGS_DECL;
   const int M = A->P.M;
   const size_t ea = (size_t)env * Q_N;
   const size_t ag = ea + d;
@@ -3073,9 +2841,8 @@ swarm_step16q(const S64Args args) {
   uint32_t gse = 0u;
   {
     const uint32_t* src = lane < 3 ? reinterpret_cast<const uint32_t*>(A->S.goal) + 3 * env + lane
-                                   : (lane == 3 ? reinterpret_cast<const uint32_t*>(A->S.step_count) + env
-                                                : A->S.episode + env);
-    if (lane < 5) gse = *src;
+                                   : reinterpret_cast<const uint32_t*>(A->S.step_count) + env;
+    if (lane < 4) gse = *src;
   }
   float ax = A->actions[ag * 3], ay = A->actions[ag * 3 + 1], az = A->actions[ag * 3 + 2];
   float px = A->S.pos[ag * 3], py = A->S.pos[ag * 3 + 1], pz = A->S.pos[ag * 3 + 2];
@@ -3092,44 +2859,8 @@ swarm_step16q(const S64Args args) {
   float gy = __uint_as_float(__builtin_amdgcn_readlane(gse, 1));
   float gz = __uint_as_float(__builtin_amdgcn_readlane(gse, 2));
   const int stepc = (int)__builtin_amdgcn_readlane(gse, 3);
-  const uint32_t episode0 = (uint32_t)__builtin_amdgcn_readlane(gse, 4);
   const int n_active = __popcll(__ballot(act) & Q_LEAD);
   STAMP_AT(env, 1);
-  SWARM_LAT_REFETCH(A);
-#if SWARM_Q16_FLOOR
-  {  // diagnostic bytes-only floor (tools: the achievable time of a one-wave-per-SIMD launch that
-     // moves this step's bytes): every input read above, every output written below in the
-     // product's store pattern, no pair / obstacle / reward / reset / finish work (wrong values)
-    const float f = ax + ay + az + gx + gy + gz + (float)stepc + (float)episode0 + (float)n_active;
-    if (q == 0) {
-      A->O.reward[ag] = f;
-      float* pe = A->S.pos + ag * 3;
-      float* ve = A->S.vel + ag * 3;
-      pe[0] = px; pe[1] = py; pe[2] = pz;
-      ve[0] = vx + f; ve[1] = vy; ve[2] = vz;
-    }
-    if (lane == 0) { A->O.env_done[env] = (uint8_t)f; A->S.step_count[env] = stepc + 1; }
-    const uint64_t m = __ballot(act && has);
-    if ((lane >> 2) < 3) {
-      uint8_t* base = (lane >> 2) == 0 ? A->O.terminated : ((lane >> 2) == 1 ? A->O.truncated : A->S.active);
-      *reinterpret_cast<uint32_t*>(base + ea + 4 * (lane & 3)) = (uint32_t)(m >> (16 * (lane & 3)));
-    }
-    wave_sync();
-    float* row = reinterpret_cast<float*>(L.stage) + d * Q_D;
-#pragma unroll
-    for (int c = 0; c < 9; ++c) row[q * 9 + c] = px + (float)c;
-    if (q == 0) row[36] = py;
-    wave_sync();
-    constexpr int V4 = Q_N * Q_D / 4;
-    const float4 v0 = L.stage[lane], v1 = L.stage[lane + 64];
-    const float4 v2 = L.stage[lane + 128 < V4 ? lane + 128 : V4 - 1];
-    float* ob = A->O.obs + ea * Q_D;
-    store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)lane, v0);
-    store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)(lane + 64), v1);
-    if (lane + 128 < V4) store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)(lane + 128), v2);
-    return;
-  }
-#endif
 
   // ---- integrate: drone_swarm_env.py:98-117 (swarm_kernel, DYN_KIN)
   float prev_d = 0.f;
@@ -3173,7 +2904,6 @@ swarm_step16q(const S64Args args) {
   put(act ? 1.f : 0.f);
   wave_sync();
   STAMP_AT(env, 2);
-  SWARM_LAT_REFETCH(A);
 
   // ---- pair + obstacle passes
   uint32_t nk[KS], ok[MSL];
@@ -3188,7 +2918,6 @@ swarm_step16q(const S64Args args) {
   else q16_pair_pass<1, false>(L.soa, d, q, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, esum);
   obstacle_pass_s64<MSL, true>(L.osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
   STAMP_AT(env, 3);
-  SWARM_LAT_REFETCH(A);
 
   // ---- rewards / terminations: drone_swarm_env.py:120-172 (swarm_kernel, DYN_KIN)
   bool pcoll;
@@ -3250,87 +2979,11 @@ swarm_step16q(const S64Args args) {
                                    (do_reset ? SWARM_ENV_RESET : 0u));
   const uint64_t m_term = __ballot(term), m_trunc = __ballot(trunc);
   STAMP_AT(env, 4);
-  SWARM_LAT_REFETCH(A);
 
-  // ---- in-kernel auto-reset (wave-uniform): new episode, then its key passes
-  uint32_t episode_new = episode0;
-  bool dkey = true;
-  if constexpr (SPEC) {
-    if (A->P.auto_reset) {
-      if (lane == 0) decision = do_reset ? 1u : 0u;
-      __syncthreads();  // wave 1 holds the next episode: it emits it when the env resets
-    }
-    if (do_reset) {  // this wave's remaining outputs: the terminated / truncated / active rows
-      s64_gu8* p_term = (s64_gu8*)A->O.terminated;
-      s64_gu8* p_trunc = (s64_gu8*)A->O.truncated;
-      s64_gu8* p_act = (s64_gu8*)A->S.active;
-      asm volatile("" : "+s"(p_term), "+s"(p_trunc), "+s"(p_act));
-      const int grp = lane >> 2;
-      if (grp < 3) {
-        const uint64_t m = grp == 0 ? m_term : (grp == 1 ? m_trunc : ~0ull);
-        const uint32_t nib = (uint32_t)(m >> (16 * (lane & 3)));
-        const uint32_t word = (nib & 1u) | ((nib >> 4) & 1u) << 8 | ((nib >> 8) & 1u) << 16 | ((nib >> 12) & 1u) << 24;
-        s64_gu8* base = grp == 0 ? p_term : (grp == 1 ? p_trunc : p_act);
-        *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(base + ea + 4 * (lane & 3)) = word;
-      }
-      return;
-    }
-  } else if (do_reset) {
-    const long long genv = A->P.env_offset + env;
-    episode_new = episode0 + 1u;
-    Q16_FLAG(4u);
-    // one Philox block per lane: quarters 0 / 1 drone d, quarter 2 obstacle d (d < M), quarter 3
-    // the goal (block N + M) — the blocks of swarm_kernel's draw_env, one round of the generator
-    // instead of two per lane
-    const uint32_t blk = q < 2 ? (uint32_t)d : (q == 2 ? (uint32_t)(Q_N + d) : (uint32_t)(Q_N + M));
-    uint32_t wv[4];
-    draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, blk, wv);
-    const float lo_w = A->P.neg_half_w, wd_w = A->P.width_w;
-    const float ux = uni(wv[0], lo_w, wd_w), uy = uni(wv[1], lo_w, wd_w), uz = uni(wv[2], lo_w, wd_w);
-    px = quad_bcast<0>(ux);
-    py = quad_bcast<0>(uy);
-    pz = quad_bcast<0>(uz);
-    vx = vy = vz = 0.f;
-    act = true;
-    wave_sync();  // every read of the old ring / obstacles is done
-    if (q == 2 && d < M) {
-      L.obst[d] = make_float4(ux, uy, uz, 0.f);
-      L.osoa[d] = ux; L.osoa[Q_MMAX + d] = uy; L.osoa[2 * Q_MMAX + d] = uz;
-    }
-    gx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ux), 3));
-    gy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(uy), 3));
-    gz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(uz), 3));
-    put(1.f);
-    wave_sync();
-#pragma unroll
-    for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
-#pragma unroll
-    for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
-    float s2 = 0.f, e2 = 0.f;
-    bool c2 = false;
-    q16_pair_pass<0, true>(L.soa, d, q, px, py, pz, true, A->P.nb_keep, 0.f, nk, s2, e2);
-    obstacle_pass_s64<MSL, false>(L.osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
-    dkey = false;  // PASS 0 ranks by s'
-  }
-  STAMP_AT(env, 5);
-  SWARM_LAT_REFETCH(A);
-
-  // ---- exact top-K: quarter q finishes neighbour slot q (q < 3) and obstacle slot q
-  float nd, ndx, ndy, ndz, od, odx, ody, odz;
-  q16_finish(A, L, d, q, M, nk, ok, dkey, px, py, pz, nd, ndx, ndy, ndz, od, odx, ody, odz);
-  STAMP_AT(env, 6);
-  SWARM_LAT_REFETCH(A);
-
-  // ---- state write-back (quarter 0), byte rows from ballots, env scalars (lane 0)
-  const bool new_act = do_reset || cont;
-  if (q == 0) {
-    float* pe = A->S.pos + ag * 3;
-    float* ve = A->S.vel + ag * 3;
-    pe[0] = px; pe[1] = py; pe[2] = pz;
-    ve[0] = vx; ve[1] = vy; ve[2] = vz;
-  }
+  // ---- the terminated / truncated / active rows: three dword rows built from ballots (a resetting
+  // env's drones are all active again)
   {
-    const uint64_t m_act = __ballot(new_act);
+    const uint64_t m_act = __ballot(do_reset || cont);
     // global-typed: made opaque, a plain pointer loses its address space and the row store becomes
     // a flat store, which every later `s_waitcnt lgkmcnt` (the obs stage) would also wait for
     s64_gu8* p_term = (s64_gu8*)A->O.terminated;
@@ -3346,18 +2999,29 @@ swarm_step16q(const S64Args args) {
       *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(base + ea + 4 * (lane & 3)) = word;
     }
   }
-  if (lane == 0) {
-    A->S.step_count[env] = do_reset ? 0 : new_step;
-    if (do_reset) {
-      A->S.episode[env] = episode_new;
-      A->S.goal[3 * env + 0] = gx; A->S.goal[3 * env + 1] = gy; A->S.goal[3 * env + 2] = gz;
-    }
+
+  // ---- auto-reset: wave 1 has drawn the next episode and prepared its observation; it emits it
+  // (state, global state, obs rows) when the env resets
+  if (A->P.auto_reset) {
+    if (lane == 0) decision = do_reset ? 1u : 0u;
+    __syncthreads();
   }
-  if (do_reset && lane < M) {
-    float* o = A->S.obstacles + ((size_t)env * M + lane) * 3;
-    const float4 qo = L.obst[lane];
-    o[0] = qo.x; o[1] = qo.y; o[2] = qo.z;
+  if (do_reset) return;
+  STAMP_AT(env, 5);
+
+  // ---- exact top-K: quarter q finishes neighbour slot q (q < 3) and obstacle slot q
+  float nd, ndx, ndy, ndz, od, odx, ody, odz;
+  q16_finish(A, L, d, q, M, nk, ok, true, px, py, pz, nd, ndx, ndy, ndz, od, odx, ody, odz);
+  STAMP_AT(env, 6);
+
+  // ---- state write-back (quarter 0), env scalars (lane 0)
+  if (q == 0) {
+    float* pe = A->S.pos + ag * 3;
+    float* ve = A->S.vel + ag * 3;
+    pe[0] = px; pe[1] = py; pe[2] = pz;
+    ve[0] = vx; ve[1] = vy; ve[2] = vz;
   }
+  if (lane == 0) A->S.step_count[env] = new_step;
   if (A->O.global_state && q == 0) {
     float* gs = A->O.global_state + (size_t)env * (6 * Q_N + 3);
     gs[3 * d] = px; gs[3 * d + 1] = py; gs[3 * d + 2] = pz;
@@ -3365,23 +3029,18 @@ swarm_step16q(const S64Args args) {
     if (d == 0) { gs[6 * Q_N + 0] = gx; gs[6 * Q_N + 1] = gy; gs[6 * Q_N + 2] = gz; }
   }
   STAMP_AT(env, 7);
-  SWARM_LAT_REFETCH(A);
 
   // ---- observation rows: staged in LDS, stored as coalesced 16-B stores
   q16_stage_row(L, d, q, px, py, pz, vx, vy, vz, gx, gy, gz, nd, ndx, ndy, ndz, od, odx, ody, odz);
   q16_store_obs(A, L, ea, lane);
   STAMP_AT(env, 8);
-#ifdef SWARM_STAMPS
-  if (lane == 0 && env < (1 << 16)) g_stamps[env * 16 + 12] = __builtin_amdgcn_s_memrealtime();
-  {
-    uint32_t fw = 0u;
-#pragma unroll
-    for (uint32_t bit = 1u; bit <= 16u; bit <<= 1)
-      fw |= __ballot((q16_flags & bit) != 0u) != 0 ? bit : 0u;
-    if (lane == 0 && env < (1 << 16)) g_stamps[env * 16 + 13] = fw;
-  }
-#endif
+  STAMP_END(env, lane == 0);
+  Q16_FLAGS_END(env, lane);
 }
+}  // namespace
+namespace swarm_dev {
+
+#endif  // SWARM_HAS_PART(6)
 
 // ------------------------------------------------------------------ step256: config 5 (N = 256)
 // Specialisation of the step for one env of exactly 256 drones per 256-thread workgroup (wave w
@@ -3403,17 +3062,11 @@ swarm_step16q(const S64Args args) {
 // the exact finish.  The keys' inserts are as many as before (each drone ranks 255 candidates);
 // distances, square roots and formation terms halve.
 constexpr int H_N = 256;
-constexpr int H_K = 3;
-constexpr int H_MS = 4;
+[[maybe_unused]] constexpr int H_K = 3;
+[[maybe_unused]] constexpr int H_MS = 4;
 constexpr int H_MMAX = 16;
 constexpr int H_BL = 128;       // per-block plane segment: 64 drones + their wrap copy
-#ifndef SWARM_H_BATCH
-#define SWARM_H_BATCH 8
-#endif
-constexpr int H_BATCH = SWARM_H_BATCH;  // rotations per scheduling batch of the pair passes
-#ifndef SWARM_H_SPLIT
-#define SWARM_H_SPLIT 0
-#endif
+constexpr int H_BATCH = H_BATCH_C;  // rotations per scheduling batch of the pair passes
 
 struct H256Lds {
   // SoA planes per block: seg[b][plane][u], planes x, y, z, eligibility; drone 64b + u at u and
@@ -3642,22 +3295,6 @@ __device__ __forceinline__ void h_pass0(H256Lds& L, int w, int t, float px, floa
   h_bases(L, w, t, A0, A1);
   h_bases(L, b1, t, B0, B1);
   h_bases(L, b2, t, C0, C1);
-#if SWARM_H_SPLIT
-  // two own lists (own block + block w + 2 / block w + 1) and the own block's mirrors in a third:
-  // every rotation feeds two independent insert chains, merged once at the end
-  uint32_t nb[4], km[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) { nb[s] = KEY_EMPTY; km[s] = KEY_EMPTY; }
-  h_seg0<31, 1, 0, 0, true>(A0, A1, t4, px, py, pz, keep, nk, km);
-  h_seg0<32, 32, 0, 0, false>(A0, A1, t4, px, py, pz, keep, nk, km);
-  h_seg0<63, 0, 64, 192, true>(B0, B1, t4, px, py, pz, keep, nb, kb);
-  if (w < 2)
-    h_seg0<31, 0, 128, 128, true>(C0, C1, t4, px, py, pz, keep, nk, kc);
-  else
-    h_seg0<32, 1, 128, 128, true>(C0, C1, t4, px, py, pz, keep, nk, kc);
-  h_merge4(nk, nb);
-  h_merge4(nk, km);
-#else
   h_seg0<31, 1, 0, 0, true>(A0, A1, t4, px, py, pz, keep, nk, nk);
   h_seg0<32, 32, 0, 0, false>(A0, A1, t4, px, py, pz, keep, nk, nk);
   // block (w, w + 1): own code 64 + r (block delta 1); mirror code 192 + (64 - r) % 64 (delta -1)
@@ -3667,7 +3304,6 @@ __device__ __forceinline__ void h_pass0(H256Lds& L, int w, int t, float px, floa
     h_seg0<31, 0, 128, 128, true>(C0, C1, t4, px, py, pz, keep, nk, kc);
   else
     h_seg0<32, 1, 128, 128, true>(C0, C1, t4, px, py, pz, keep, nk, kc);
-#endif
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     L.x.keys[0][s][64 * b1 + t] = kb[s];
@@ -3731,41 +3367,11 @@ __device__ __forceinline__ uint32_t h_finish_fast(const uint32_t (&nk)[4], const
 
 // Phase stamps of step256 (diagnostic stamps build, tools/stamps.py with SWARM_STAMPS_KERNEL=n256):
 // wave 0's view of each phase boundary, one record per env
-#ifdef SWARM_STAMPS
-#define STAMP256(i)                                                                      \
-  do {                                                                                   \
-    __builtin_amdgcn_sched_barrier(0);                                                   \
-    unsigned long long ts_;                                                              \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts_)::"memory");           \
-    __builtin_amdgcn_sched_barrier(0);                                                   \
-    if (threadIdx.x == 0 && env < (1 << 16)) g_stamps[env * 16 + (i)] = ts_;             \
-  } while (0)
-#else
-#define STAMP256(i) do {} while (0)
-#endif
-// swarm_step256s's LDS (the kernel is below, after swarm_step256)
-struct H256SLds {
-  float seg[4][4][H_BL];  // the step's planes (x, y, z, eligibility), as H256Lds
-  float4 ring[H_N];
-  float4 obst[H_MMAX];
-  float osoa[3 * H_MMAX];
-  uint32_t red[4];
-  struct {
-    float sum[2][H_N];
-    float mn[2][H_N];
-  } p1;
-  // the next episode: x / y / z planes (every new drone is active: no eligibility plane)
-  float sseg[4][3][H_BL];
-  float4 sring[H_N];
-  float4 sobst[H_MMAX];
-  float sosoa[3 * H_MMAX];
-  float4 sgoal;
-  uint32_t keys[2][4][H_N];  // key lists handed to another wave's drones (the next episode's pass,
-                             // then a continuing env's pass after the decision)
-};
-static_assert(sizeof(H256SLds) * 4 <= 160 * 1024, "four 512-thread workgroups per CU");
+#define STAMP256(i) STAMP_AT(threadIdx.x == 0 ? env : (1 << 16), i)
 
 #if SWARM_HAS_PART(7)  // emitted in its own translation unit only
+}  // namespace swarm_dev
+namespace {  // kernels: internal to this translation unit
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) swarm_step256(const S64Args args) {
   (void)args;  // read through s64_args()
   constexpr int KS = H_K + 1, MSL = H_MS + 1;
@@ -3778,9 +3384,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   const int M = A->P.M;
   const size_t ag = (size_t)env * H_N + i;
   STAMP256(0);
-#ifdef SWARM_STAMPS
-  if (i == 0 && env < (1 << 16)) g_stamps[env * 16 + 11] = __builtin_amdgcn_s_memrealtime();
-#endif
+  STAMP_BEGIN(env, i == 0);
 
   // ---- loads
   const float gx0 = A->S.goal[3 * env], gy0 = A->S.goal[3 * env + 1], gz0 = A->S.goal[3 * env + 2];
@@ -3839,27 +3443,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   // ---- formation + minimum pass (every pair once), obstacle pass
   double fsum = 0.0;
   float smin = __builtin_inff();
-#if SWARM_DIAG_EXTRA_INT
-  {  // diagnostic: SWARM_DIAG_EXTRA_INT dependent-free v_min_u32 / v_max_u32 per wave
-    uint32_t z0 = __float_as_uint(px), z1 = __float_as_uint(py), z2 = __float_as_uint(pz), z3 = (uint32_t)t;
-#pragma unroll
-    for (int q = 0; q < SWARM_DIAG_EXTRA_INT / 4; ++q) {
-      z0 = min(z0, z1); z1 = max(z1, z2); z2 = min(z2, z3); z3 = max(z3, z0);
-      asm volatile("" : "+v"(z0), "+v"(z1), "+v"(z2), "+v"(z3));
-    }
-    if (z0 + z1 + z2 + z3 == 12345u) fsum += 1.0;
-  }
-#endif
-#if SWARM_DIAG_EXTRA_VALU
-  {  // diagnostic: SWARM_DIAG_EXTRA_VALU dependent-free v_mul_f32 per wave
-    float z0 = px, z1 = py, z2 = pz, z3 = px + 1.f;
-#pragma unroll
-    for (int q = 0; q < SWARM_DIAG_EXTRA_VALU / 4; ++q) {
-      z0 = z0 * 0.999f; z1 = z1 * 0.999f; z2 = z2 * 0.999f; z3 = z3 * 0.999f;
-    }
-    if (z0 + z1 + z2 + z3 == 1234.5f) fsum += 1.0;
-  }
-#endif
   if (fast) h_pass1<true>(L.seg, L.x.p1.sum, L.x.p1.mn, w, t, true, px, py, pz, A->P.ds_f, fsum, smin);
   else h_pass1<false>(L.seg, L.x.p1.sum, L.x.p1.mn, w, t, act, px, py, pz, A->P.ds_f, fsum, smin);
   uint32_t ok[MSL];
@@ -4041,345 +3624,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     row[21 + 4 * s] = q.x - px; row[22 + 4 * s] = q.y - py; row[23 + 4 * s] = q.z - pz; row[24 + 4 * s] = od[s];
   }
   STAMP256(8);
-#ifdef SWARM_STAMPS
-  if (i == 0 && env < (1 << 16)) {
-    g_stamps[env * 16 + 9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
-    g_stamps[env * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-    g_stamps[env * 16 + 12] = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
+  STAMP_END(env, i == 0);
 }
+}  // namespace
+namespace swarm_dev {
 
-// ---- step256 with next-episode waves: one env per 512-thread workgroup
-// A reset is deterministic before the step decides it: the next episode's drones, obstacles and
-// goal are Philox4x32-10(seed, global env, episode + 1) draws (drone_swarm_env.py:65-90).  Waves
-// 0-3 step the env as swarm_step256 does (integrate, the formation / minimum pass, rewards and
-// terminations); waves 4-7 meanwhile draw the next episode and run its keys pass, obstacle keys
-// and exact finish, so a resetting env's observation is ready when the reset is decided and the
-// two halves of a resetting env's work (at N = 256 with the default radii, nearly every env every
-// step) run side by side instead of one after the other, at 8 waves per SIMD instead of 4.  A
-// continuing env's keys pass still runs after the decision, on waves 0-3 (as in swarm_step256).
-// Every output is the one swarm_step256 writes, bit for bit (same helpers, same order per drone).
-
-// h_pass0 over a given plane set, handing the other waves' lists through `keys`
-template <int NP>
-__device__ __forceinline__ void hs_pass0(float (*seg)[NP][H_BL], uint32_t (*keys)[4][H_N], int w, int t, float px,
-                                         float py, float pz, uint32_t keep, uint32_t (&nk)[4]) {
-  const int b1 = (w + 1) & 3, b2 = (w + 2) & 3;
-  const uint32_t t4 = (uint32_t)t << 2;
-  uint32_t kb[4], kc[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) { kb[s] = KEY_EMPTY; kc[s] = KEY_EMPTY; }
-  s64_lds_cf *A0, *A1, *B0, *B1, *C0, *C1;
-  h_bases_p<NP>(seg, w, t, A0, A1);
-  h_bases_p<NP>(seg, b1, t, B0, B1);
-  h_bases_p<NP>(seg, b2, t, C0, C1);
-  h_seg0<31, 1, 0, 0, true>(A0, A1, t4, px, py, pz, keep, nk, nk);
-  h_seg0<32, 32, 0, 0, false>(A0, A1, t4, px, py, pz, keep, nk, nk);
-  h_seg0<63, 0, 64, 192, true>(B0, B1, t4, px, py, pz, keep, nk, kb);
-  if (w < 2)
-    h_seg0<31, 0, 128, 128, true>(C0, C1, t4, px, py, pz, keep, nk, kc);
-  else
-    h_seg0<32, 1, 128, 128, true>(C0, C1, t4, px, py, pz, keep, nk, kc);
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    keys[0][s][64 * b1 + t] = kb[s];
-    keys[1][s][64 * b2 + t] = kc[s];
-  }
-}
-// after the barrier: merge the two handed-over lists of drone i = 64 w + t, decode the codes
-__device__ __forceinline__ void hs_merge(uint32_t (*keys)[4][H_N], int i, int w, int t, uint32_t keep,
-                                         uint32_t (&nk)[4]) {
-  uint32_t kb[4], kc[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) { kb[s] = keys[0][s][i]; kc[s] = keys[1][s][i]; }
-  h_merge4(nk, kb);
-  h_merge4(nk, kc);
-#pragma unroll
-  for (int s = 0; s < 4; ++s) nk[s] = h_decode(nk[s], w, t, keep);
-}
-// the exact top-K of the emitted observation (swarm_step256's finish)
-__device__ __forceinline__ void hs_finish(S64ArgPtr A, const float4* __restrict__ ring, const float4* __restrict__ obst,
-                                          int i, int M, const uint32_t (&nk)[4], const uint32_t (&ok)[5], float px,
-                                          float py, float pz, float (&wd)[4], int (&wj)[4], float (&od)[5],
-                                          int (&oj)[5]) {
-  constexpr int KS = H_K + 1, MSL = H_MS + 1;
-  const uint32_t ff = h_finish_fast(nk, ok, ring, obst, M, A->P.nb_keep, A->P.ob_keep, px, py, pz, wd, wj, od, oj);
-  if (__ballot(ff != 0) != 0) {
-    bool slow_nb, slow_ob;
-    s64_finish_general<KS, MSL, H_N, false, H_MMAX>(ff, nk, ok, ring, obst, i, M, A->P.nb_keep, A->P.ob_keep, false,
-                                                    px, py, pz, wd, wj, od, oj, slow_nb, slow_ob);
-    if (slow_nb) exact_select<KS, false>(ring, H_N, i, H_K, max_first(wd, H_K), px, py, pz, wd, wj);
-    if (slow_ob) exact_select<MSL, true>(obst, M, -1, H_MS, max_first(od, H_MS), px, py, pz, od, oj);
-  }
-}
-// state write-back + global state + observation row of drone i (swarm_step256's, in its order)
-__device__ __forceinline__ void hs_emit(S64ArgPtr A, int env, int i, int M, const float4* __restrict__ ring,
-                                        const float4* __restrict__ obst, const float (&wd)[4], const int (&wj)[4],
-                                        const float (&od)[5], const int (&oj)[5], float px, float py, float pz,
-                                        float vx, float vy, float vz, float gx, float gy, float gz, bool new_act,
-                                        bool do_reset, int new_step, uint32_t episode_new) {
-  const size_t ag = (size_t)env * H_N + i;
-  A->S.pos[ag * 3] = px; A->S.pos[ag * 3 + 1] = py; A->S.pos[ag * 3 + 2] = pz;
-  A->S.vel[ag * 3] = vx; A->S.vel[ag * 3 + 1] = vy; A->S.vel[ag * 3 + 2] = vz;
-  A->S.active[ag] = new_act ? 1 : 0;
-  if (i == 0) {
-    A->S.step_count[env] = do_reset ? 0 : new_step;
-    if (do_reset) {
-      A->S.episode[env] = episode_new;
-      A->S.goal[3 * env] = gx; A->S.goal[3 * env + 1] = gy; A->S.goal[3 * env + 2] = gz;
-    }
-  }
-  if (do_reset && i < M) {
-    float* o = A->S.obstacles + ((size_t)env * M + i) * 3;
-    const float4 q = obst[i];
-    o[0] = q.x; o[1] = q.y; o[2] = q.z;
-  }
-  if (A->O.global_state) {
-    float* gs = A->O.global_state + (size_t)env * (6 * H_N + 3);
-    gs[3 * i] = px; gs[3 * i + 1] = py; gs[3 * i + 2] = pz;
-    gs[3 * H_N + 3 * i] = vx; gs[3 * H_N + 3 * i + 1] = vy; gs[3 * H_N + 3 * i + 2] = vz;
-    if (i == 0) { gs[6 * H_N] = gx; gs[6 * H_N + 1] = gy; gs[6 * H_N + 2] = gz; }
-  }
-  float* row = A->O.obs + ag * (9 + 4 * H_K + 4 * H_MS);
-  row[0] = px; row[1] = py; row[2] = pz;
-  row[3] = vx; row[4] = vy; row[5] = vz;
-  row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
-#pragma unroll
-  for (int s = 0; s < H_K; ++s) {
-    const float4 q = lds_f4(ring + (wj[s] & (H_N - 1)));
-    row[9 + 4 * s] = q.x - px; row[10 + 4 * s] = q.y - py; row[11 + 4 * s] = q.z - pz; row[12 + 4 * s] = wd[s];
-  }
-#pragma unroll
-  for (int s = 0; s < H_MS; ++s) {
-    const float4 q = lds_f4(obst + (oj[s] & (H_MMAX - 1)));
-    row[21 + 4 * s] = q.x - px; row[22 + 4 * s] = q.y - py; row[23 + 4 * s] = q.z - pz; row[24 + 4 * s] = od[s];
-  }
-}
-
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) swarm_step256s(const S64Args args) {
-  (void)args;  // read through s64_args()
-  constexpr int MSL = H_MS + 1;
-  __shared__ H256SLds L;
-  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const bool spec = wv >= 4;           // waves 4-7: the next episode
-  const int w = wv & 3, t = threadIdx.x & 63;
-  const int i = 64 * w + t;            // drone
-  S64ArgPtr A = s64_args();
-  const int env = blockIdx.x;
-  if (env >= A->P.E) return;  // whole block
-  if (spec && !A->P.auto_reset) return;  // no reset can follow: nothing to prepare
-  const int M = A->P.M;
-  const size_t ag = (size_t)env * H_N + i;
-  const int stepc = A->S.step_count[env];
-  const uint32_t episode0 = A->S.episode[env];
-
-  if (spec) {
-    // ---- the next episode: draws (swarm_step256's reset block), planes, obstacles, goal
-    const uint32_t episode_new = episode0 + 1u;
-    const long long genv = A->P.env_offset + env;
-    float px, py, pz;
-    {
-      uint32_t wd4[4], wo[4];
-      draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)i, wd4);
-      const bool drawer = i <= M;  // obstacle i (i < M) or the goal (i == M)
-      if (drawer) draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)(H_N + i), wo);
-      const float lo_w = A->P.neg_half_w, wd_w = A->P.width_w;
-      px = uni(wd4[0], lo_w, wd_w);
-      py = uni(wd4[1], lo_w, wd_w);
-      pz = uni(wd4[2], lo_w, wd_w);
-      if (drawer) {
-        const float ox = uni(wo[0], lo_w, wd_w), oy = uni(wo[1], lo_w, wd_w), oz = uni(wo[2], lo_w, wd_w);
-        if (i < M) {
-          L.sobst[i] = make_float4(ox, oy, oz, 0.f);
-          L.sosoa[i] = ox; L.sosoa[H_MMAX + i] = oy; L.sosoa[2 * H_MMAX + i] = oz;
-        } else {
-          L.sgoal = make_float4(ox, oy, oz, 0.f);
-        }
-      }
-      L.sseg[w][0][t] = px; L.sseg[w][0][t + 64] = px;
-      L.sseg[w][1][t] = py; L.sseg[w][1][t + 64] = py;
-      L.sseg[w][2][t] = pz; L.sseg[w][2][t + 64] = pz;
-      L.sring[i] = make_float4(px, py, pz, 1.f);
-    }
-    const int n_active = __syncthreads_count(false);  // barrier 1 (the step's active count)
-    (void)__syncthreads_and(true);                     // barrier 2: the next episode's planes are in
-    A = s64_args();
-    uint32_t nk[4], ok[MSL];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) nk[s] = KEY_EMPTY;
-#pragma unroll
-    for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
-    bool c2 = false;
-    obstacle_pass_s64<MSL, false>(L.sosoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
-    hs_pass0<3>(L.sseg, L.keys, w, t, px, py, pz, A->P.nb_keep, nk);
-    __syncthreads();  // barrier 3: handed-over key lists written
-    A = s64_args();
-    hs_merge(L.keys, i, w, t, A->P.nb_keep, nk);
-    float wd[4], od[MSL];
-    int wj[4], oj[MSL];
-    hs_finish(A, L.sring, L.sobst, i, M, nk, ok, px, py, pz, wd, wj, od, oj);
-    __syncthreads();  // barrier 4: the step's votes are in (and every read of `keys` is done)
-    A = s64_args();
-    const uint32_t votes = L.red[0] | L.red[1] | L.red[2] | L.red[3];
-    const bool any_c = (votes & 1u) != 0, any_cand = (votes & 2u) != 0;
-    bool term_all = false, trunc_all = false;
-    if (n_active == 0) {
-      term_all = true;
-    } else {
-      const bool tl = stepc + 1 >= A->P.max_steps;
-      term_all = (!any_cand && !any_c && !tl) || any_c;
-      trunc_all = tl && !term_all;
-    }
-    if (!(term_all || trunc_all)) return;  // a continuing env: waves 0-3 emit it
-    const float4 g4 = L.sgoal;
-    hs_emit(A, env, i, M, L.sring, L.sobst, wd, wj, od, oj, px, py, pz, 0.f, 0.f, 0.f, g4.x, g4.y, g4.z, true, true, 0,
-            episode_new);
-    return;
-  }
-
-  // ---- waves 0-3: the step (swarm_step256's phases up to the reset decision)
-  const float gx = A->S.goal[3 * env], gy = A->S.goal[3 * env + 1], gz = A->S.goal[3 * env + 2];
-  float ax = A->actions[ag * 3], ay = A->actions[ag * 3 + 1], az = A->actions[ag * 3 + 2];
-  float px = A->S.pos[ag * 3], py = A->S.pos[ag * 3 + 1], pz = A->S.pos[ag * 3 + 2];
-  float vx = A->S.vel[ag * 3], vy = A->S.vel[ag * 3 + 1], vz = A->S.vel[ag * 3 + 2];
-  bool act = A->S.active[ag] != 0;
-  const bool has = A->amask == nullptr || A->amask[ag] != 0;
-  if (i < M) {
-    const float* o = A->S.obstacles + ((size_t)env * M + i) * 3;
-    const float ox = o[0], oy = o[1], oz = o[2];
-    L.obst[i] = make_float4(ox, oy, oz, 0.f);
-    L.osoa[i] = ox; L.osoa[H_MMAX + i] = oy; L.osoa[2 * H_MMAX + i] = oz;
-  }
-  const int n_active = __syncthreads_count(act);  // barrier 1
-  A = s64_args();
-  float prev_d = 0.f;
-  if (act) {
-    prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
-    if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
-    ax = clampf(ax, -1.f, 1.f) * A->P.amax;
-    ay = clampf(ay, -1.f, 1.f) * A->P.amax;
-    az = clampf(az, -1.f, 1.f) * A->P.amax;
-    vx = vx + ax * A->P.dt;
-    vy = vy + ay * A->P.dt;
-    vz = vz + az * A->P.dt;
-    const float s_sp = sqsum_1d(vx, vy, vz);
-    if (!(s_sp <= A->P.s_vmax)) {
-      const float sp = sqrt_rn(s_sp);
-      if (!(sp <= A->P.vmax || sp < (float)1e-8)) {
-        vx = (vx / sp) * A->P.vmax;
-        vy = (vy / sp) * A->P.vmax;
-        vz = (vz / sp) * A->P.vmax;
-      }
-    }
-    px = px + vx * A->P.dt;
-    py = py + vy * A->P.dt;
-    pz = pz + vz * A->P.dt;
-  }
-  if (n_active > 0) {
-    px = clampf(px, A->P.neg_half_w, A->P.half_w);
-    py = clampf(py, A->P.neg_half_w, A->P.half_w);
-    pz = clampf(pz, A->P.neg_half_w, A->P.half_w);
-  }
-  {
-    const float el = act ? 1.f : 0.f;
-    L.seg[w][0][t] = px; L.seg[w][0][t + 64] = px;
-    L.seg[w][1][t] = py; L.seg[w][1][t + 64] = py;
-    L.seg[w][2][t] = pz; L.seg[w][2][t + 64] = pz;
-    L.seg[w][3][t] = el; L.seg[w][3][t + 64] = el;
-    L.ring[i] = make_float4(px, py, pz, el);
-  }
-  const bool fast = __syncthreads_and(act) != 0;  // barrier 2
-  A = s64_args();
-
-  // ---- formation + minimum pass (every pair once), obstacle pass (swarm_step256's)
-  double fsum = 0.0;
-  float smin = __builtin_inff();
-  if (fast) h_pass1<true>(L.seg, L.p1.sum, L.p1.mn, w, t, true, px, py, pz, A->P.ds_f, fsum, smin);
-  else h_pass1<false>(L.seg, L.p1.sum, L.p1.mn, w, t, act, px, py, pz, A->P.ds_f, fsum, smin);
-  uint32_t ok[MSL];
-#pragma unroll
-  for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
-  bool ocoll = false;
-  obstacle_pass_s64<MSL, true>(L.osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
-  __syncthreads();  // barrier 3: handed-over sums / minima written
-  fsum += (double)L.p1.sum[0][i];
-  fsum += (double)L.p1.sum[1][i];
-  smin = fminf(smin, fminf(L.p1.mn[0][i], L.p1.mn[1][i]));
-  A = s64_args();
-
-  // ---- rewards / terminations: drone_swarm_env.py:120-172 (swarm_step256's)
-  bool pcoll = smin <= A->P.thr_pair * FAST_LO;
-  if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act)
-    pcoll = exact_pair_collision(L.ring, H_N, i, px, py, pz, A->P.s_pair);
-  const float curr = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
-  float rew = 0.f;
-  bool reached = false, collided = false, term = false, trunc = false, cont = false;
-  bool term_all = false, trunc_all = false;
-  int new_step = stepc;
-  bool p_coll = false, p_cand = false;
-  if (act) {
-    reached = (double)curr <= A->P.goal_radius;
-    collided = ocoll || pcoll;
-    p_coll = collided;
-    p_cand = !reached && !collided;
-    double r = ((double)prev_d - (double)curr) * A->P.kp;
-    if (n_active > 1) r = r + (-A->P.kf) * (fsum * inv_count(n_active - 1));
-    if (reached) r = r + A->P.r_goal;
-    if (collided) r = r + A->P.r_col;
-    rew = (float)r;
-  }
-  {
-    const bool wc = __ballot(p_coll) != 0, wdv = __ballot(p_cand) != 0;
-    if (t == 0) L.red[w] = (wc ? 1u : 0u) | (wdv ? 2u : 0u);
-  }
-  __syncthreads();  // barrier 4
-  const uint32_t votes = L.red[0] | L.red[1] | L.red[2] | L.red[3];
-  const bool any_c = (votes & 1u) != 0, any_cand = (votes & 2u) != 0;
-  A = s64_args();
-  if (n_active == 0) {
-    term_all = true;
-  } else {
-    new_step = stepc + 1;
-    const bool tl = new_step >= A->P.max_steps;
-    term_all = (!any_cand && !any_c && !tl) || any_c;
-    trunc_all = tl && !term_all;
-    if (act) {
-      const bool done_i = reached || collided;
-      term = done_i;
-      trunc = tl && !done_i;
-      cont = !done_i && !tl && !any_c;
-    }
-  }
-  const bool do_reset = A->P.auto_reset && (term_all || trunc_all);
-  A->O.reward[ag] = rew;
-  A->O.terminated[ag] = term ? 1 : 0;
-  A->O.truncated[ag] = trunc ? 1 : 0;
-  if (A->O.dist_goal) A->O.dist_goal[ag] = curr;
-  if (A->O.info_flags)
-    A->O.info_flags[ag] = (uint8_t)((act ? SWARM_AGENT_STEPPED : 0u) | (act && reached ? SWARM_AGENT_REACHED : 0u) |
-                                    (act && collided ? SWARM_AGENT_COLLISION : 0u) | (cont ? SWARM_AGENT_HAS_OBS : 0u));
-  if (i == 0)
-    A->O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
-                                   (do_reset ? SWARM_ENV_RESET : 0u));
-  if (do_reset) return;  // waves 4-7 emit the next episode
-
-  // ---- a continuing env (or no auto-reset): its keys pass on the emitted positions, then the
-  // finish and the write-back (waves 4-7 have left or are leaving: the barrier counts waves 0-3)
-  uint32_t nk[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) nk[s] = KEY_EMPTY;
-  hs_pass0<4>(L.seg, L.keys, w, t, px, py, pz, A->P.nb_keep, nk);
-  __syncthreads();  // barrier 5 (waves 0-3)
-  A = s64_args();
-  hs_merge(L.keys, i, w, t, A->P.nb_keep, nk);
-  float wd[4], od[MSL];
-  int wj[4], oj[MSL];
-  hs_finish(A, L.ring, L.obst, i, M, nk, ok, px, py, pz, wd, wj, od, oj);
-  A = s64_args();
-  hs_emit(A, env, i, M, L.ring, L.obst, wd, wj, od, oj, px, py, pz, vx, vy, vz, gx, gy, gz, cont, false, new_step,
-          episode0);
-}
 #endif
 
 // ------------------------------------------------------------------ host side
@@ -4420,7 +3669,7 @@ void* pick_lm(int lm, int ks, int msl) {
 #endif
 }
 
-}  // namespace
+}  // namespace swarm_dev
 
 // kernel tables, one per translation unit (SWARM_PART); returns the host stub of the kernel
 #define SWARM_PICK_DECL(k) __attribute__((visibility("hidden"))) void* swarm_pick_##k(int lm, int ks, int msl)
@@ -4432,17 +3681,15 @@ SWARM_PICK_DECL(3);
 __attribute__((visibility("hidden"))) void* swarm_pick_step64(bool persistent, bool physics);
 __attribute__((visibility("hidden"))) void* swarm_pick_step64_eval();
 // the config-2 specialisation (SWARM_PART 6)
-__attribute__((visibility("hidden"))) void* swarm_pick_step16q(bool spec);
+__attribute__((visibility("hidden"))) void* swarm_pick_step16q();
 // the config-5 specialisation (SWARM_PART 7)
 __attribute__((visibility("hidden"))) void* swarm_pick_step256();
-__attribute__((visibility("hidden"))) void* swarm_pick_step256s();  // 512-thread, next-episode waves
 #if SWARM_HAS_PART(7)
 __attribute__((visibility("hidden"))) void* swarm_pick_step256() { return reinterpret_cast<void*>(swarm_step256); }
-__attribute__((visibility("hidden"))) void* swarm_pick_step256s() { return reinterpret_cast<void*>(swarm_step256s); }
 #endif
 #if SWARM_HAS_PART(6)
-__attribute__((visibility("hidden"))) void* swarm_pick_step16q(bool spec) {
-  return spec ? reinterpret_cast<void*>(swarm_step16q<1, true>) : reinterpret_cast<void*>(swarm_step16q<Q_WG_ENVS>);
+__attribute__((visibility("hidden"))) void* swarm_pick_step16q() {
+  return reinterpret_cast<void*>(swarm_step16q);
 }
 #endif
 #if SWARM_HAS_PART(5)
@@ -4531,15 +3778,6 @@ bool step64_applies(const swarm_params_t* p, const KParams& k) {
          k.M <= S64_MMAX && (p->dynamics == DYN_KIN || p->dynamics == DYN_PHYS);
 }
 
-// step16q's 2-wave launch (the next episode prepared by a second wave) unless SWARM_STEP16Q_SPEC=0
-// selects the one-wave-per-env launch (read once per process)
-bool step16q_spec() {
-  static const bool on = []() {
-    const char* v = getenv("SWARM_STEP16Q_SPEC");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
 // The config-2 specialisation swarm_step16q covers N = 16, K = 3, Ms = 4, 4 <= M <= 16, kinematic.
 bool step16q_applies(const swarm_params_t* p, const KParams& k) {
   return p->kernel_path == SWARM_PATH_AUTO && k.N == Q_N && k.K == Q_K && k.Ms == Q_MS && k.M >= Q_MS &&
@@ -4547,15 +3785,6 @@ bool step16q_applies(const swarm_params_t* p, const KParams& k) {
 }
 
 // The config-5 specialisation swarm_step256 covers N = 256, K = 3, Ms = 4, 4 <= M <= 16, kinematic.
-// diagnostic: SWARM_STEP256_SPEC=1 selects swarm_step256s (512 threads: the step on waves 0-3,
-// the next episode on waves 4-7; measured slower, r05c) instead of swarm_step256 (read once)
-bool step256_spec() {
-  static const bool on = []() {
-    const char* v = getenv("SWARM_STEP256_SPEC");
-    return v && v[0] == '1';
-  }();
-  return on;
-}
 bool step256_applies(const swarm_params_t* p, const KParams& k) {
   return p->kernel_path == SWARM_PATH_AUTO && k.N == H_N && k.K == H_K && k.Ms == H_MS && k.M >= H_MS &&
          k.M <= H_MMAX && p->dynamics == DYN_KIN;
@@ -4806,24 +4035,17 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   if (mode == MODE_STEP && step16q_applies(p, kp) && !s->env_cfg && ((uintptr_t)o->obs) % 16 == 0 &&
       ((uintptr_t)o->terminated | (uintptr_t)o->truncated | (uintptr_t)s->active) % 4 == 0) {
     const S64Args args{kp, *s, actions, amask, *o, ev};
-    if (step16q_spec())  // one env per 2-wave workgroup: wave 1 prepares the next episode
-      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step16q(true)), dim3(kp.E), dim3(128), 0,
-                         (hipStream_t)stream, args);
-    else
-      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step16q(false)),
-                         dim3((kp.E + Q_WG_ENVS - 1) / Q_WG_ENVS), dim3(64 * Q_WG_ENVS), 0, (hipStream_t)stream, args);
+    // one env per 2-wave workgroup: wave 1 prepares the next episode
+    hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step16q()), dim3(kp.E), dim3(128), 0,
+                       (hipStream_t)stream, args);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SWARM_OK;
   }
   if (mode == MODE_STEP && step256_applies(p, kp) && !s->env_cfg) {
     const S64Args args{kp, *s, actions, amask, *o};
-    if (step256_spec())
-      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step256s()), dim3(kp.E), dim3(2 * H_N), 0,
-                         (hipStream_t)stream, args);
-    else
-      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step256()), dim3(kp.E), dim3(H_N), 0,
-                         (hipStream_t)stream, args);
+    hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step256()), dim3(kp.E), dim3(H_N), 0,
+                       (hipStream_t)stream, args);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SWARM_OK;
@@ -4961,20 +4183,19 @@ int swarm_query_launch(const swarm_params_t* p, swarm_launch_info_t* info) {
   const int rc = build_kparams(p, &kp, info);
   if (rc == SWARM_OK && step16q_applies(p, kp)) {  // one env per 64-lane wave, 4 lanes per drone
     info->lanes_per_env = 64;
-    const bool spec = step16q_spec();
-    info->threads_per_block = spec ? 128 : 64 * Q_WG_ENVS;
-    info->envs_per_block = spec ? 1 : Q_WG_ENVS;
-    info->blocks = spec ? kp.E : (kp.E + Q_WG_ENVS - 1) / Q_WG_ENVS;
-    info->lds_bytes = spec ? 2 * (int)sizeof(Q16Lds) + 4 : Q_WG_ENVS * (int)sizeof(Q16Lds);
+    info->threads_per_block = 128;  // wave 0 steps the env, wave 1 prepares its next episode
+    info->envs_per_block = 1;
+    info->blocks = kp.E;
+    info->lds_bytes = 2 * (int)sizeof(Q16Lds) + 4;
     info->staged_obs = 0;
     info->kernel_id = SWARM_KERNEL_STEP16Q;
   }
-  if (rc == SWARM_OK && step256_applies(p, kp)) {  // one env per workgroup, one lane per drone (+ next-episode waves)
+  if (rc == SWARM_OK && step256_applies(p, kp)) {  // one env per 256-thread workgroup, one lane per drone
     info->lanes_per_env = H_N;
-    info->threads_per_block = step256_spec() ? 2 * H_N : H_N;
+    info->threads_per_block = H_N;
     info->envs_per_block = 1;
     info->blocks = kp.E;
-    info->lds_bytes = step256_spec() ? (int)sizeof(H256SLds) : (int)sizeof(H256Lds);
+    info->lds_bytes = (int)sizeof(H256Lds);
     info->staged_obs = 0;
     info->kernel_id = SWARM_KERNEL_STEP256;
   }
