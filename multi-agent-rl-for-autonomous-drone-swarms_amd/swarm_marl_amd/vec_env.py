@@ -605,7 +605,7 @@ class VecSwarm:
         if kid == nat.KERNEL_STEP64_PERSISTENT and self.persistent:
             return "swarm_step64<32>"
         if kid == nat.KERNEL_STEP16Q:
-            return "swarm_step16q<4>"
+            return "swarm_step16q"
         if kid == nat.KERNEL_STEP256:
             return "swarm_step256"
         if kid in (nat.KERNEL_STEP64, nat.KERNEL_STEP64_PERSISTENT):

@@ -53,7 +53,7 @@ def test_kernel_selection(dev):
     from swarm_marl_amd import VecSwarm
     from swarm_marl_amd import _native as nat
     v = VecSwarm(8, {"num_drones": 16}, device=dev)
-    assert int(v.launch_info.kernel_id) == nat.KERNEL_STEP16Q and v.kernel_name() == "swarm_step16q<4>"
+    assert int(v.launch_info.kernel_id) == nat.KERNEL_STEP16Q and v.kernel_name() == "swarm_step16q"
     for raw in ({"num_drones": 15}, {"num_drones": 16, "neighbor_k": 4}, {"num_drones": 16, "sensed_obstacles": 3},
                 {"num_drones": 16, "num_obstacles": 3}, {"num_drones": 16, "num_obstacles": 17}):
         assert int(VecSwarm(4, raw, device=dev).launch_info.kernel_id) == nat.KERNEL_GENERIC, raw
@@ -69,7 +69,7 @@ def test_step16q_matches_generic_autoreset(dev, m, max_steps, masked):
     raw = dict(num_drones=16, num_obstacles=m, max_steps=max_steps)
     e = 1023  # ragged last workgroup
     a, b = _pair(dev, raw, e, auto_reset=True, seed=5, env_offset=3)
-    assert a.kernel_name() == "swarm_step16q<4>"
+    assert a.kernel_name() == "swarm_step16q"
     a.reset()
     b.reset()
     _assert_same(a, b, "reset")
@@ -137,7 +137,7 @@ def test_step16q_vs_oracle(dev):
     cfg = oracle_cfg(raw)
     e = 96
     vec = VecSwarm(e, raw, device=dev, auto_reset=True, seed=21, with_infos=True, with_global_state=True)
-    assert vec.kernel_name() == "swarm_step16q<4>"
+    assert vec.kernel_name() == "swarm_step16q"
     vec.reset()
     torch.cuda.synchronize()
     st = vec_state_numpy(vec)
