@@ -466,6 +466,7 @@ constexpr float X3_LO_SCALE = 2048.f, X3_LO_INV = 1.f / 2048.f;
 #define SWARM_POLICY_X3_BATCH 8
 #endif
 constexpr int X3_B = SWARM_POLICY_X3_BATCH;  // W2 k-steps per lo-fragment batch (divides 16)
+constexpr int X3_DEPTH = 2;  // W2 lo batches in flight (3 / 4 measured no faster, r05k)
 // Tried and measured slower or equal: three accumulator chains (hi*lo and
 // lo*hi apart), layer-3 lo fragments requested a block early, W1 / W3 lo fragments a block ahead,
 // the next tile's observations prefetched into registers (spills) or touched into L2, and the
@@ -591,10 +592,20 @@ policy_mlp_x3(const FwdArgs A) {
         }
     }
     // ---- layer 1: 256 x (in + 1), relu -> h1 hi / lo (16 k-step fragments each)
+    // software pipelined like layer 2 below: block ob - 1's epilogue (x3_sum, relu + split into
+    // two h1 k-step fragments) interleaved with block ob's nine MFMAs
     f16x8 h1h[KS2], h1l[KS2];
+    f32x16 l1acc[2], l1accx[2];
+    auto epi1 = [&](int pob, int part) {
+      if (part == 0) l1acc[pob & 1] = x3_sum(l1acc[pob & 1], l1accx[pob & 1]);
+      else split8(l1acc[pob & 1], part - 1, true, h1h[2 * pob + part - 1], h1l[2 * pob + part - 1]);
+    };
 #pragma unroll
     for (int ob = 0; ob < OB; ++ob) {
-      f32x16 acc = f32x16{}, accx = f32x16{};
+      f32x16& acc = l1acc[ob & 1];
+      f32x16& accx = l1accx[ob & 1];
+      acc = f32x16{};
+      accx = f32x16{};
       f16x8 w1l[KS1];
 #pragma unroll
       for (int ks = 0; ks < KS1; ++ks) w1l[ks] = wlo_load(WL, lb, sb + (uint32_t)(L.w1 + (size_t)(ob * KS1 + ks) * FRAG));
@@ -602,12 +613,13 @@ policy_mlp_x3(const FwdArgs A) {
       for (int ks = 0; ks < KS1; ++ks) {
         if (X3_ABL & 8) acc[ks] += (float)w1f[(ob * KS1 + ks) * 64][0] * (float)w1l[ks][1] + (float)xh[ks][2] + (float)xl[ks][3];
         else mfma3(w1f[(ob * KS1 + ks) * 64], w1l[ks], xh[ks], xl[ks], acc, accx);
+        if (ob > 0) epi1(ob - 1, ks);
       }
-      acc = x3_sum(acc, accx);
-      split8(acc, 0, true, h1h[2 * ob], h1l[2 * ob]);
-      split8(acc, 1, true, h1h[2 * ob + 1], h1l[2 * ob + 1]);
       __builtin_amdgcn_sched_barrier(0);
     }
+    epi1(OB - 1, 0);
+    epi1(OB - 1, 1);
+    epi1(OB - 1, 2);
     // ---- layer 2 (relu) fused with layer 3: each out block's two split fragments feed layer 3's
     // k-steps 2ob, 2ob+1 at once
     f32x16 acc3, acc3x = f32x16{};
@@ -619,12 +631,41 @@ policy_mlp_x3(const FwdArgs A) {
     // W2 lo fragments stream in batches of X3_B k-steps, double-buffered: batch b + 1's loads are
     // issued before batch b's MFMAs (128 fragments per wave in (ob, ks) order)
     constexpr int NB2 = OB * KS2 / X3_B;
-    f16x8 wlb[2][X3_B];
+    constexpr int DEP = X3_DEPTH;  // batches in flight: batch b + DEP - 1 is requested before batch b's MFMAs
+    f16x8 wlb[DEP][X3_B];
 #pragma unroll
-    for (int u = 0; u < X3_B; ++u) wlb[0][u] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)u * FRAG));
+    for (int b0 = 0; b0 + 1 < DEP; ++b0)
+#pragma unroll
+      for (int u = 0; u < X3_B; ++u) wlb[b0][u] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)(b0 * X3_B + u) * FRAG));
+    // Software pipeline over the out blocks: block ob's layer-2 MFMAs accumulate into one of two
+    // accumulator pairs while the epilogue of block ob - 1 (x3_sum, relu + hi / lo split, its two
+    // layer-3 k-steps) is interleaved with block ob's first batch — at one wave per SIMD nothing
+    // else would fill the MFMA pipe during that vector work.
+    f32x16 acc2[2], accx2[2];
+    f32x16 pacc;           // block ob - 1's layer-2 output
+    f16x8 a0h = {}, a1h = {}, a0l = {}, a1l = {};
+    auto epi = [&](int pob, int part) {  // a third of block pob's epilogue
+      if (part == 0) {
+        pacc = x3_sum(acc2[pob & 1], accx2[pob & 1]);
+        if (w3lane) {  // this block's layer-3 fragments (k-steps 2pob, 2pob+1), the lo halves from L2
+          a0h = w3f[(2 * pob) * 2 * out + w3idx];
+          a1h = w3f[(2 * pob + 1) * 2 * out + w3idx];
+          a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * pob) * 2 * out * 16));
+          a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * pob + 1) * 2 * out * 16));
+        }
+      } else {
+        f16x8 h2h, h2l;
+        split8(pacc, part - 1, true, h2h, h2l);
+        if (X3_ABL & 16) acc3[part - 1] += (float)a0h[0] * (float)a0l[1] + (float)h2h[2] + (float)h2l[3];
+        else if (part == 1) mfma3(a0h, a0l, h2h, h2l, acc3, acc3x);
+        else mfma3(a1h, a1l, h2h, h2l, acc3, acc3x);
+      }
+    };
 #pragma unroll
     for (int ob = 0; ob < OB; ++ob) {
-      f32x16 acc, accx = f32x16{};
+      f32x16& acc = acc2[ob & 1];
+      f32x16& accx = accx2[ob & 1];
+      accx = f32x16{};
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 b = *reinterpret_cast<const float4*>(b2 + ob * 32 + 8 * g + 4 * h);
@@ -633,41 +674,29 @@ policy_mlp_x3(const FwdArgs A) {
 #pragma unroll
       for (int kb = 0; kb < KS2; kb += X3_B) {
         const int bi = (ob * KS2 + kb) / X3_B;  // batch index
-        if (bi + 1 < NB2 && !(X3_ABL & 1)) {
+        const int nb = bi + DEP - 1;  // the batch requested now
+        if (nb < NB2 && !(X3_ABL & 1)) {
 #pragma unroll
           for (int u = 0; u < X3_B; ++u)
-            wlb[(bi + 1) & 1][u] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)((bi + 1) * X3_B + u) * FRAG));
+            wlb[nb % DEP][u] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)(nb * X3_B + u) * FRAG));
         }
         f16x8 wh[X3_B];
 #pragma unroll
-        for (int u = 0; u < X3_B; ++u) wh[u] = (X3_ABL & 2) ? wlb[bi & 1][u] : w2f[(ob * KS2 + kb + u) * 64];
-        if (!(X3_ABL & 4)) {
+        for (int u = 0; u < X3_B; ++u) wh[u] = (X3_ABL & 2) ? wlb[bi % DEP][u] : w2f[(ob * KS2 + kb + u) * 64];
 #pragma unroll
-          for (int u = 0; u < X3_B; ++u)
-            mfma3(wh[u], (X3_ABL & 1) ? wh[u] : wlb[bi & 1][u], h1h[kb + u], h1l[kb + u], acc, accx);
-        } else {
-#pragma unroll
-          for (int u = 0; u < X3_B; ++u) acc[u] += (float)wh[u][0] * (float)wlb[bi & 1][u][1] + (float)h1h[kb + u][2] + (float)h1l[kb + u][3];
+        for (int u = 0; u < X3_B; ++u) {
+          if (!(X3_ABL & 4)) mfma3(wh[u], (X3_ABL & 1) ? wh[u] : wlb[bi % DEP][u], h1h[kb + u], h1l[kb + u], acc, accx);
+          else acc[u] += (float)wh[u][0] * (float)wlb[bi % DEP][u][1] + (float)h1h[kb + u][2] + (float)h1l[kb + u][3];
+          // the previous block's epilogue, in thirds after k-steps 1, 3 and 5 of the block
+          if (ob > 0 && kb + u < 6 && (kb + u) % 2 == 1) epi(ob - 1, (kb + u) / 2);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      acc = x3_sum(acc, accx);
-      f16x8 a0h = {}, a1h = {}, a0l = {}, a1l = {};
-      if (w3lane) {  // this block's layer-3 fragments (k-steps 2ob, 2ob+1), the lo halves from L2
-        a0h = w3f[(2 * ob) * 2 * out + w3idx];
-        a1h = w3f[(2 * ob + 1) * 2 * out + w3idx];
-        a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob) * 2 * out * 16));
-        a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob + 1) * 2 * out * 16));
-      }
-      f16x8 h2h, h2l;
-      split8(acc, 0, true, h2h, h2l);
-      if (X3_ABL & 16) acc3[0] += (float)a0h[0] * (float)a0l[1] + (float)h2h[2] + (float)h2l[3];
-      else mfma3(a0h, a0l, h2h, h2l, acc3, acc3x);
-      split8(acc, 1, true, h2h, h2l);
-      if (X3_ABL & 16) acc3[1] += (float)a1h[0] * (float)a1l[1] + (float)h2h[2] + (float)h2l[3];
-      else mfma3(a1h, a1l, h2h, h2l, acc3, acc3x);
-      __builtin_amdgcn_sched_barrier(0);
     }
+    // the last block's epilogue
+    epi(OB - 1, 0);
+    epi(OB - 1, 1);
+    epi(OB - 1, 2);
     acc3 = x3_sum(acc3, acc3x);
     // ---- outputs: lane holds logits m = (i&3) + 8(i>>2) + 4h of its row (out <= 12: i < 8)
     if (A.logits && valid) {
