@@ -5,12 +5,14 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=${1:-r02}
 export TMPDIR=/tmp
+# PMC_SETS (optional): counter groups separated by ';' instead of the default four passes
+if [ -n "${PMC_SETS:-}" ]; then IFS=';' read -r -a SETS <<< "$PMC_SETS"; else SETS=(
+    "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
+    "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
+    "FETCH_SIZE" "WRITE_SIZE"); fi
 for c in ${CONFIGS:-headline n16 n256}; do
   i=0
-  for set in \
-    "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
-    "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE" \
-    "FETCH_SIZE" "WRITE_SIZE"; do
+  for set in "${SETS[@]}"; do
     i=$((i+1))
     d=gpurun_out/$R/pmc_$c/p$i
     mkdir -p $d

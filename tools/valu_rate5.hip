@@ -28,7 +28,6 @@ KERNEL(k_bperm, INIT, "ds_bpermute_b32 v14, v16, v12", CL)
 KERNEL(k_read2, INIT, "ds_read2_b32 v[14:15], v16 offset1:1", CL)
 KERNEL(k_readb128, INIT, "ds_read_b128 v[16:19], v14", CL)
 KERNEL(k_snop, INIT, "s_nop 0", CL)
-KERNEL(k_salu, INIT, "s_add_u32 s20, s20, 1", CL)
 
 int main() {
   float* out;
@@ -38,7 +37,7 @@ int main() {
       {"v_cndmask_e64 s[]", k_cnd_s}, {"v_cmp vcc + v_cndmask vcc (pair)", k_cmp_cnd},
       {"v_cmp s[] + v_cndmask s[] (pair)", k_cmp_cnd64}, {"v_cmp -> vcc", k_cmpvcc}, {"v_cmp -> s[]", k_cmps},
       {"v_add_co_u32 (vcc carry)", k_addc}, {"ds_bpermute_b32", k_bperm}, {"ds_read2_b32", k_read2},
-      {"ds_read_b128", k_readb128}, {"s_nop 0", k_snop}, {"s_add_u32", k_salu}};
+      {"ds_read_b128", k_readb128}, {"s_nop 0", k_snop}};
   const int blocks = 256 * 8;
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
