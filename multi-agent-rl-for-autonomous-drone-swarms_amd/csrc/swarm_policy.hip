@@ -462,30 +462,15 @@ typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
 typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr float X3_LO_SCALE = 2048.f, X3_LO_INV = 1.f / 2048.f;
-#ifndef SWARM_POLICY_X3_BATCH
-#define SWARM_POLICY_X3_BATCH 8
-#endif
-constexpr int X3_B = SWARM_POLICY_X3_BATCH;  // W2 k-steps per lo-fragment batch (divides 16)
+constexpr int X3_B = 8;      // W2 k-steps per lo-fragment batch (divides 16; 4 measured slower, r05k)
 constexpr int X3_DEPTH = 2;  // W2 lo batches in flight (3 / 4 measured no faster, r05k)
 // Tried and measured slower or equal: three accumulator chains (hi*lo and
 // lo*hi apart), layer-3 lo fragments requested a block early, W1 / W3 lo fragments a block ahead,
 // the next tile's observations prefetched into registers (spills) or touched into L2, and the
 // out-block epilogues software-pipelined into the next block's MFMAs with sched_group_barrier.
 
-// diagnostic ablations (timing only, wrong logits): 1 no W2 lo loads (hi used), 2 no W2 hi LDS
-// reads (lo used), 4 no layer-2 MFMAs, 8 no layer-1 MFMAs, 16 no layer-3 MFMAs, 32 splits as plain
-// f16 conversions
-#ifndef X3_ABL
-#define X3_ABL 0
-#endif
 // 8 accumulator values (sub-block s) -> hi / lo f16 fragments, relu'd first when `act`
 __device__ __forceinline__ void split8(const f32x16& a, int s, bool act, f16x8& hi, f16x8& lo) {
-  if (X3_ABL & 32) {  // diagnostic: f16 conversion only (no relu, no lo part)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) hi[q] = (_Float16)a[8 * s + q];
-    lo = hi;
-    return;
-  }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     float x0 = a[8 * s + 2 * q], x1 = a[8 * s + 2 * q + 1];
@@ -611,8 +596,7 @@ policy_mlp_x3(const FwdArgs A) {
       for (int ks = 0; ks < KS1; ++ks) w1l[ks] = wlo_load(WL, lb, sb + (uint32_t)(L.w1 + (size_t)(ob * KS1 + ks) * FRAG));
 #pragma unroll
       for (int ks = 0; ks < KS1; ++ks) {
-        if (X3_ABL & 8) acc[ks] += (float)w1f[(ob * KS1 + ks) * 64][0] * (float)w1l[ks][1] + (float)xh[ks][2] + (float)xl[ks][3];
-        else mfma3(w1f[(ob * KS1 + ks) * 64], w1l[ks], xh[ks], xl[ks], acc, accx);
+        mfma3(w1f[(ob * KS1 + ks) * 64], w1l[ks], xh[ks], xl[ks], acc, accx);
         if (ob > 0) epi1(ob - 1, ks);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -656,8 +640,7 @@ policy_mlp_x3(const FwdArgs A) {
       } else {
         f16x8 h2h, h2l;
         split8(pacc, part - 1, true, h2h, h2l);
-        if (X3_ABL & 16) acc3[part - 1] += (float)a0h[0] * (float)a0l[1] + (float)h2h[2] + (float)h2l[3];
-        else if (part == 1) mfma3(a0h, a0l, h2h, h2l, acc3, acc3x);
+        if (part == 1) mfma3(a0h, a0l, h2h, h2l, acc3, acc3x);
         else mfma3(a1h, a1l, h2h, h2l, acc3, acc3x);
       }
     };
@@ -675,18 +658,17 @@ policy_mlp_x3(const FwdArgs A) {
       for (int kb = 0; kb < KS2; kb += X3_B) {
         const int bi = (ob * KS2 + kb) / X3_B;  // batch index
         const int nb = bi + DEP - 1;  // the batch requested now
-        if (nb < NB2 && !(X3_ABL & 1)) {
+        if (nb < NB2) {
 #pragma unroll
           for (int u = 0; u < X3_B; ++u)
             wlb[nb % DEP][u] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)(nb * X3_B + u) * FRAG));
         }
         f16x8 wh[X3_B];
 #pragma unroll
-        for (int u = 0; u < X3_B; ++u) wh[u] = (X3_ABL & 2) ? wlb[bi % DEP][u] : w2f[(ob * KS2 + kb + u) * 64];
+        for (int u = 0; u < X3_B; ++u) wh[u] = w2f[(ob * KS2 + kb + u) * 64];
 #pragma unroll
         for (int u = 0; u < X3_B; ++u) {
-          if (!(X3_ABL & 4)) mfma3(wh[u], (X3_ABL & 1) ? wh[u] : wlb[bi % DEP][u], h1h[kb + u], h1l[kb + u], acc, accx);
-          else acc[u] += (float)wh[u][0] * (float)wlb[bi % DEP][u][1] + (float)h1h[kb + u][2] + (float)h1l[kb + u][3];
+          mfma3(wh[u], wlb[bi % DEP][u], h1h[kb + u], h1l[kb + u], acc, accx);
           // the previous block's epilogue, in thirds after k-steps 1, 3 and 5 of the block
           if (ob > 0 && kb + u < 6 && (kb + u) % 2 == 1) epi(ob - 1, (kb + u) / 2);
         }
@@ -724,23 +706,15 @@ policy_mlp_x3(const FwdArgs A) {
   }
 }
 
-#ifndef SWARM_POLICY_WAVES
-#define SWARM_POLICY_WAVES 8
-#endif
-constexpr int BF16_WAVES = SWARM_POLICY_WAVES;  // T = 1: waves per workgroup (one workgroup per CU: the LDS blob)
-#ifndef SWARM_POLICY_TILES
-#define SWARM_POLICY_TILES 1
-#endif
-constexpr int BF16_TILES = SWARM_POLICY_TILES;            // row tiles per wave
-constexpr int BF16_WAVES_T = BF16_TILES > 1 ? 4 : BF16_WAVES;  // T = 2: one wave per SIMD
+// bf16: 8 waves per workgroup (one workgroup per CU: the LDS blob), one 32-row tile per wave (12 /
+// 16 waves and two tiles per wave measured slower)
+constexpr int BF16_TILES = 1;
+constexpr int BF16_WAVES_T = 8;
 constexpr int F32_WAVES = 4;
-#ifndef SWARM_POLICY_X3_WAVES
-#define SWARM_POLICY_X3_WAVES 4
-#endif
 // f32x3: waves per workgroup (one workgroup per CU: the LDS blob); 4 = one wave per SIMD: the hi
 // and lo fragments of h1 (128 VGPRs), three accumulator chains and the double-buffered W2 lo
 // batches need ~330 registers (at 2 waves per SIMD, 256, it spills)
-constexpr int X3_WAVES = SWARM_POLICY_X3_WAVES;
+constexpr int X3_WAVES = 4;
 
 thread_local char g_perr[256] = "";
 int pfail(int code, const char* msg) {

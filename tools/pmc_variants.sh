@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC of diagnostic library variants (tools/variants.sh -> build/var/<name>.so) on the headline
+# PMC of diagnostic library variants (tools/variants_fast.sh -> build/var/<name>.so) on the headline
 # shape, one counter pass per variant:  bash tools/pmc_variants.sh <tag> <name> ...
 #   -> gpurun_out/<tag>/pmc_<name>/
 # COUNTERS overrides the default set (LDS bank conflicts + issue counts).

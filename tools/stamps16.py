@@ -1,5 +1,5 @@
 """Per-wave lifetimes of swarm_step16q over many steps, with the slow paths each wave took
-(diagnostic; a full -DSWARM_STAMPS build, e.g. tools/variants.sh stamps16:-DSWARM_STAMPS):
+(diagnostic; a full -DSWARM_STAMPS build, e.g. tools/variants_fast.sh with -DSWARM_STAMPS):
     SWARM_STAMPS_LIB=build/var/stamps16.so python tools/stamps16.py [E] [steps]
 Flags: 1 / 16 quad exact-selection finish of the neighbours / obstacles (near-tie or unproven bound),
 2 exact pair-collision band, 4 reset, 8 masked pass."""
