@@ -104,6 +104,7 @@ struct KParams {
   float thr_pair, s_pair, s_obst;   // kinematic: distance threshold, squared-space thresholds
   float thr_ppair, s_phys_pair, s_phys_obst, ground_z;
   float h, g, gcomp;
+  float s_goal;  // largest s with (double)sqrt_rn(s) <= goal_radius (step16q's reached test)
   double goal_radius, kp, r_goal, r_col, kf, vmax_d;
 };
 
@@ -2492,8 +2493,13 @@ namespace swarm_dev {
 //    merged across the quad with two DPP bitonic merges (12 min/max each), formation partial sums
 //    and running minima with two DPP reductions;
 //  * finish: quarter q computes the exact distance of neighbour slot q and obstacle slot q;
-//  * observation row: quarter q stores its slots' 4-float groups, quarter 3 also p, v, g - p,
-//    straight from registers (no LDS stage: the launch is latency-bound).
+//  * observation row: quarter q stages its slots' 4-float groups, quarter 3 also p, v, g - p, in
+//    LDS; the env's rows leave as coalesced 16-B stores.
+// Three waves per env (192-thread workgroup): waves 0 and 1 both load and integrate the env, then
+// wave 0 runs the formation / running-minimum pass, the obstacle collisions, rewards,
+// terminations, flags and state, while wave 1 runs the keys pass, the exact finish and the
+// observation rows of the continuing env; wave 2 prepares the next episode (q16_next_episode).
+// One workgroup barrier hands wave 0's reset decision to waves 1 and 2.
 // Integrate, obstacle pass, rewards and terminations run redundantly on the four lanes of a
 // drone (identical values); every per-drone output is written by quarter 0.  Same numerics as
 // swarm_kernel<0, 0, 4, 5, 1> (the generic kernel at N = 16), obs bit-identical
@@ -2518,6 +2524,29 @@ union Q16Lds {
 };
 
 #if SWARM_HAS_PART(6)  // step16q's device code: its own translation unit
+// step16q's leading kernel arguments: the addresses of the loads the integrate waits for, which
+// the gfx950 kernarg preload puts in SGPRs at wave start (this translation unit is built with
+// -amdgpu-kernarg-preload-count=16; 14 user SGPRs are left for it): those global loads issue
+// without a scalar load of the kernarg segment first.  The S64Args block follows them at byte
+// offset Q16_HOT_BYTES.  The launch is exactly E workgroups (no bounds test: it would wait for a
+// kernarg load before the first global load).
+struct Q16Hot {
+  const float* pos;
+  const float* vel;
+  const float* actions;
+  const uint8_t* active;
+  const uint32_t* goal;
+  const int32_t* step_count;
+  const uint8_t* amask;  // NULL: every agent has an action
+};
+constexpr uint32_t Q16_HOT_BYTES = 56;
+static_assert(alignof(S64Args) <= 8, "S64Args at kernarg offset 56");
+__device__ __forceinline__ S64ArgPtr q16_args() {
+  uint64_t v = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr()) + Q16_HOT_BYTES;
+  asm volatile("" : "+s"(v));
+  return reinterpret_cast<S64ArgPtr>(v);
+}
+
 // DPP quad permutations: xor 1, xor 2, broadcast of quad lane k
 __device__ __forceinline__ uint32_t quad_xor1(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false); }
 __device__ __forceinline__ uint32_t quad_xor2(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false); }
@@ -2585,11 +2614,15 @@ __device__ __forceinline__ void q16_quad_select4(q16_key (&k)[4]) {
 }
 
 // One quarter's share of the symmetric pair pass of drone d: rotations q + 1 and q + 5 (r = 8 has
-// no mirror).  PASS 1: d~ keys + formation + running minimum (non-FAST); PASS 0: s' keys only.
-template <int PASS, bool FAST>
+// no mirror).  PASS 1: d~ values; PASS 0: s' keys only.  KEYS: the top-4 key list (merged over the
+// quad); FORM (PASS 1): formation sum and running minimum (the minimum also on FAST passes without
+// keys, where no nearest key decides the pair collision).
+template <int PASS, bool FAST, bool KEYS = true, bool FORM = true>
 __device__ __forceinline__ void q16_pair_pass(const float* __restrict__ soa, int d, int q, float px, float py, float pz,
                                               bool self, uint32_t keep, float ds, uint32_t (&nk)[4], float& smin,
                                               float& esum) {
+  constexpr bool SUMS = PASS == 1 && FORM;
+  constexpr bool MINS = SUMS && (!FAST || !KEYS);
   const uint32_t sflag = (FAST || self) ? 0u : 0x80000000u;
   const uint32_t keep_m = keep & 0x7fffffffu;
 #pragma unroll
@@ -2600,30 +2633,26 @@ __device__ __forceinline__ void q16_pair_pass(const float* __restrict__ soa, int
     const float v = PASS == 1 ? __builtin_amdgcn_sqrtf(s) : s;
     const bool el = FAST || (self && soa[96 + j] != 0.f);
     // the list starts empty: inserts 1 .. 4 of the pass skip the compares against KEY_EMPTY
-    kins_n<4>(nk, (__float_as_uint(v) & keep) | (uint32_t)r, 2 * it);
-    if constexpr (PASS == 1) {
-      if constexpr (!FAST) smin = fminf(smin, el ? v : __builtin_inff());
-      esum += el ? fabsf(v - ds) : 0.f;
-    }
+    if constexpr (KEYS) kins_n<4>(nk, (__float_as_uint(v) & keep) | (uint32_t)r, 2 * it);
+    if constexpr (MINS) smin = fminf(smin, el ? v : __builtin_inff());
+    if constexpr (SUMS) esum += el ? fabsf(v - ds) : 0.f;
     // mirror: lane (d, q) receives drone (d - r)'s value of the pair (d - r, d) from lane 4(d - r) + q
     const int src = (((d - r) & (Q_N - 1)) << 2) | q;
     const uint32_t rcv = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)(__float_as_uint(v) | sflag));
     if (r < 8) {
       const float vm = __uint_as_float(rcv & 0x7fffffffu);
       const bool pr = FAST || (self && !(rcv >> 31));
-      kins_n<4>(nk, (rcv & keep_m) | (uint32_t)(Q_N - r), 2 * it + 1);
-      if constexpr (PASS == 1) {
-        if constexpr (!FAST) smin = fminf(smin, pr ? vm : __builtin_inff());
-        esum += pr ? fabsf(vm - ds) : 0.f;
-      }
+      if constexpr (KEYS) kins_n<4>(nk, (rcv & keep_m) | (uint32_t)(Q_N - r), 2 * it + 1);
+      if constexpr (MINS) smin = fminf(smin, pr ? vm : __builtin_inff());
+      if constexpr (SUMS) esum += pr ? fabsf(vm - ds) : 0.f;
     }
   }
-  quad_merge4<1>(nk);
-  quad_merge4<2>(nk);
-  if constexpr (PASS == 1) {
-    esum = quad_sum(esum);
-    if constexpr (!FAST) smin = quad_min(smin);
+  if constexpr (KEYS) {
+    quad_merge4<1>(nk);
+    quad_merge4<2>(nk);
   }
+  if constexpr (SUMS) esum = quad_sum(esum);
+  if constexpr (MINS) smin = quad_min(smin);
 }
 
 // step16q's exact top-K of the emitted observation: quarter q measures neighbour slot q (q < 3)
@@ -2728,9 +2757,9 @@ __device__ __forceinline__ void q16_store_obs(S64ArgPtr A, const Q16Lds& L, size
   if (lane + 128 < V4) store_obs(ob, Q_N * Q_D * 4, 16u * (uint32_t)(lane + 128), v2);
 }
 
-// step16q's next-episode wave (SWARM_STEP16Q 2-wave launch, wave 1 of an env's workgroup): a reset
+// step16q's next-episode wave (wave 2 of an env's workgroup): a reset
 // is deterministic before the step decides it — Philox4x32-10(seed, global env, episode + 1) —
-// so while wave 0 steps the env, this wave draws the next episode exactly as step16q's reset block
+// so while waves 0 and 1 step the env, this wave draws the next episode exactly as step16q's reset block
 // does, runs its keys passes and exact finish and stages its observation rows.  At the decision
 // (one workgroup barrier) it writes the new episode's state, global state and observations when
 // the env resets, else it leaves.  The launch is latency-bound (one wave per SIMD): the reset's
@@ -2780,7 +2809,7 @@ __device__ __forceinline__ void q16_next_episode(S64ArgPtr A, int env, int lane,
   q16_stage_row(H, d, q, px, py, pz, 0.f, 0.f, 0.f, gx, gy, gz, nd, ndx, ndy, ndz, od, odx, ody, odz);
   __syncthreads();  // wave 0's decision
   if (*reinterpret_cast<const volatile uint32_t*>(decision) == 0u) return;
-  A = s64_args();
+  A = q16_args();
   if (q == 0) {
     float* pe = A->S.pos + ag * 3;
     float* ve = A->S.vel + ag * 3;
@@ -2805,66 +2834,69 @@ __device__ __forceinline__ void q16_next_episode(S64ArgPtr A, int env, int lane,
   q16_store_obs(A, H, ea, lane);
 }
 
-// step16q (one wave per SIMD, latency-bound) reads the kernarg segment through one pointer, so
-// the compiler batches the parameter loads at the top instead of a dependent scalar round trip at
-// each phase: 6.85 -> 6.80 us (step256 measured 46.8 -> 47.5-48.2 us that way and keeps step64's
-// per-phase re-fetch).
-// 71 VGPRs without spills at 4 waves per EU (at 8: 64 VGPRs and 4 spilled, scratch round trips
-// on a latency-bound launch): config 2 (one wave per SIMD) 6.58 vs 6.85 us per step
-// One env per 2-wave workgroup: wave 0 steps the env, wave 1 runs q16_next_episode.
-}  // namespace swarm_dev
-namespace {  // kernels: internal to this translation unit
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(Q16_WAVES_PER_EU)))
-swarm_step16q(const S64Args args) {
-  (void)args;  // read through s64_args()
-  constexpr int KS = Q_K + 1, MSL = Q_MS + 1;
-  __shared__ Q16Lds ldsq[2];
-  __shared__ uint32_t decision;  // wave 0's reset decision for wave 1
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  S64ArgPtr A = s64_args();
-  const int env = blockIdx.x;
-  if (env >= A->P.E) return;  // whole workgroup
-  if (wv == 1) {
-    if (A->P.auto_reset) q16_next_episode(A, env, lane, ldsq[1], &decision);
-    return;
-  }
-  Q16Lds& L = ldsq[0];
-  const int d = lane >> 2, q = lane & 3;
-  STAMP_AT(env, 0);
-  STAMP_BEGIN(env, lane == 0);
-  Q16_FLAGS_DECL;
-  const int M = A->P.M;
-  const size_t ea = (size_t)env * Q_N;
-  const size_t ag = ea + d;
-  // ---- loads (the four lanes of a drone read the same words)
-  uint32_t gse = 0u;
-  {
-    const uint32_t* src = lane < 3 ? reinterpret_cast<const uint32_t*>(A->S.goal) + 3 * env + lane
-                                   : reinterpret_cast<const uint32_t*>(A->S.step_count) + env;
-    if (lane < 4) gse = *src;
-  }
-  float ax = A->actions[ag * 3], ay = A->actions[ag * 3 + 1], az = A->actions[ag * 3 + 2];
-  float px = A->S.pos[ag * 3], py = A->S.pos[ag * 3 + 1], pz = A->S.pos[ag * 3 + 2];
-  float vx = A->S.vel[ag * 3], vy = A->S.vel[ag * 3 + 1], vz = A->S.vel[ag * 3 + 2];
-  bool act = A->S.active[ag] != 0;
-  const bool has = A->amask == nullptr || A->amask[ag] != 0;
-  if (lane < M) {
-    const float* o = A->S.obstacles + ((size_t)env * M + lane) * 3;
-    const float ox = o[0], oy = o[1], oz = o[2];
-    L.obst[lane] = make_float4(ox, oy, oz, 0.f);
-    L.osoa[lane] = ox; L.osoa[Q_MMAX + lane] = oy; L.osoa[2 * Q_MMAX + lane] = oz;
-  }
-  float gx = __uint_as_float(__builtin_amdgcn_readlane(gse, 0));
-  float gy = __uint_as_float(__builtin_amdgcn_readlane(gse, 1));
-  float gz = __uint_as_float(__builtin_amdgcn_readlane(gse, 2));
-  const int stepc = (int)__builtin_amdgcn_readlane(gse, 3);
-  const int n_active = __popcll(__ballot(act) & Q_LEAD);
-  STAMP_AT(env, 1);
+// One env's step inputs after the integrate (the step and observation waves hold the same values).
+struct Q16Step {
+  float px, py, pz, vx, vy, vz, gx, gy, gz, prev_d;
+  int stepc, n_active;
+  bool act, fast;
+};
+// One env's loaded words, not yet used (q16_load issues every load before anything waits for one)
+struct Q16Raw {
+  float ax, ay, az, ox, oy, oz;
+  uint32_t gse, act, hm;
+};
 
-  // ---- integrate: drone_swarm_env.py:98-117 (swarm_kernel, DYN_KIN)
+// Loads (the four lanes of a drone read the same words).
+__device__ __forceinline__ void q16_load(S64ArgPtr A, const Q16Hot& H, int env, int lane, int M, Q16Step& st,
+                                         Q16Raw& w) {
+  // 32-bit element offsets (E * 16 * 37 < 2^31, step16q_applies): 64-bit index arithmetic let the
+  // register allocator tie an address's unused high half to the goal word's load register, a false
+  // dependency that made every later load wait for that one
+  const uint32_t ag = (uint32_t)env * Q_N + (uint32_t)(lane >> 2), ag3 = 3u * ag;
+  w.gse = 0u;
+  {
+    const uint32_t* src = lane < 3 ? H.goal + 3u * (uint32_t)env + (uint32_t)lane
+                                   : reinterpret_cast<const uint32_t*>(H.step_count) + (uint32_t)env;
+    if (lane < 4) w.gse = *src;
+  }
+  w.ax = H.actions[ag3]; w.ay = H.actions[ag3 + 1]; w.az = H.actions[ag3 + 2];
+  st.px = H.pos[ag3]; st.py = H.pos[ag3 + 1]; st.pz = H.pos[ag3 + 2];
+  st.vx = H.vel[ag3]; st.vy = H.vel[ag3 + 1]; st.vz = H.vel[ag3 + 2];
+  w.act = H.active[ag];
+  // unconditional (a branch on the mask pointer made the later loads wait for every load above)
+  w.hm = (H.amask != nullptr ? H.amask : H.active)[ag];
+  // every load above is addressed from preloaded SGPRs: issue them all before the first wait for
+  // a kernarg-segment scalar load (M and the obstacle base below)
+  __builtin_amdgcn_sched_barrier(0);
+  {  // obstacles (address from the kernarg segment): written to LDS after the integrate
+    const int m = lane < M ? lane : M - 1;  // lanes >= M re-load the last obstacle (unused)
+    const float* o = A->S.obstacles + 3u * ((uint32_t)env * (uint32_t)M + (uint32_t)m);
+    w.ox = o[0]; w.oy = o[1]; w.oz = o[2];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Integrate (drone_swarm_env.py:98-117, swarm_kernel DYN_KIN), then this wave's rings.
+__device__ __forceinline__ void q16_integrate(S64ArgPtr A, const Q16Hot& H, int lane, int M, Q16Lds& L, Q16Step& st,
+                                              Q16Raw w) {
+  const int d = lane >> 2, q = lane & 3;
+  // the actions and the mask byte pinned here: left to the compiler, their loads sank into the
+  // `act` branch below and issued only after the loads above had returned (a second round trip)
+  asm volatile("" : "+v"(w.ax), "+v"(w.ay), "+v"(w.az), "+v"(w.hm));
+  float ax = w.ax, ay = w.ay, az = w.az;
+  const bool has = H.amask == nullptr || w.hm != 0u;
+  st.act = w.act != 0u;
+  st.gx = __uint_as_float(__builtin_amdgcn_readlane(w.gse, 0));
+  st.gy = __uint_as_float(__builtin_amdgcn_readlane(w.gse, 1));
+  st.gz = __uint_as_float(__builtin_amdgcn_readlane(w.gse, 2));
+  st.stepc = (int)__builtin_amdgcn_readlane(w.gse, 3);
+  st.n_active = __popcll(__ballot(st.act) & Q_LEAD);
+  st.fast = (__ballot(st.act) & Q_LEAD) == Q_LEAD;
+  const float ox = w.ox, oy = w.oy, oz = w.oz;
+  float px = st.px, py = st.py, pz = st.pz, vx = st.vx, vy = st.vy, vz = st.vz;
+  const float gx = st.gx, gy = st.gy, gz = st.gz;
   float prev_d = 0.f;
-  if (act) {
+  if (st.act) {
     prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
     if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
     ax = clampf(ax, -1.f, 1.f) * A->P.amax;
@@ -2886,76 +2918,149 @@ swarm_step16q(const S64Args args) {
     py = py + vy * A->P.dt;
     pz = pz + vz * A->P.dt;
   }
-  if (n_active > 0) {
+  if (st.n_active > 0) {
     px = clampf(px, A->P.neg_half_w, A->P.half_w);
     py = clampf(py, A->P.neg_half_w, A->P.half_w);
     pz = clampf(pz, A->P.neg_half_w, A->P.half_w);
   }
-  auto put = [&](float w_el) {
-    if (q == 0) {
-      L.ring[d] = make_float4(px, py, pz, w_el);
+  if (lane < M) {
+    L.obst[lane] = make_float4(ox, oy, oz, 0.f);
+    L.osoa[lane] = ox; L.osoa[Q_MMAX + lane] = oy; L.osoa[2 * Q_MMAX + lane] = oz;
+  }
+  if (q == 0) {
+    const float w_el = st.act ? 1.f : 0.f;
+    L.ring[d] = make_float4(px, py, pz, w_el);
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        L.soa[d + 16 * c] = px; L.soa[32 + d + 16 * c] = py; L.soa[64 + d + 16 * c] = pz;
-        L.soa[96 + d + 16 * c] = w_el;
-      }
+    for (int c = 0; c < 2; ++c) {
+      L.soa[d + 16 * c] = px; L.soa[32 + d + 16 * c] = py; L.soa[64 + d + 16 * c] = pz;
+      L.soa[96 + d + 16 * c] = w_el;
     }
-  };
-  put(act ? 1.f : 0.f);
+  }
+  st.px = px; st.py = py; st.pz = pz; st.vx = vx; st.vy = vy; st.vz = vz; st.prev_d = prev_d;
   wave_sync();
-  STAMP_AT(env, 2);
+}
 
-  // ---- pair + obstacle passes
+// step16q's observation wave (wave 1): the continuing env's observation — the keys pass on the
+// post-step positions, the exact finish, the rows staged in LDS — while wave 0 computes rewards and
+// terminations; stored once wave 0's reset decision says the env continues.
+__device__ __forceinline__ void q16_obs_wave(S64ArgPtr A, int env, int lane, int M, Q16Lds& L, const Q16Step& st,
+                                             const uint32_t* decision) {
+  constexpr int KS = Q_K + 1, MSL = Q_MS + 1;
+  const int d = lane >> 2, q = lane & 3;
   uint32_t nk[KS], ok[MSL];
 #pragma unroll
   for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
 #pragma unroll
   for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
   float smin = __builtin_inff(), esum = 0.f;
-  bool ocoll = false;
-  const bool fast = (__ballot(act) & Q_LEAD) == Q_LEAD;
-  if (fast) q16_pair_pass<1, true>(L.soa, d, q, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, esum);
-  else q16_pair_pass<1, false>(L.soa, d, q, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, esum);
-  obstacle_pass_s64<MSL, true>(L.osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
-  STAMP_AT(env, 3);
+  bool unused = false;
+  if (st.fast) q16_pair_pass<1, true, true, false>(L.soa, d, q, st.px, st.py, st.pz, true, A->P.nb_keep, 0.f, nk, smin, esum);
+  else q16_pair_pass<1, false, true, false>(L.soa, d, q, st.px, st.py, st.pz, st.act, A->P.nb_keep, 0.f, nk, smin, esum);
+  obstacle_pass_s64<MSL, false>(L.osoa, M, st.px, st.py, st.pz, false, 0.f, A->P.ob_keep, ok, unused);
+  STAMP_AT(env, 5);
+  float nd, ndx, ndy, ndz, od, odx, ody, odz;
+  q16_finish(A, L, d, q, M, nk, ok, true, st.px, st.py, st.pz, nd, ndx, ndy, ndz, od, odx, ody, odz);
+  STAMP_AT(env, 6);
+  q16_stage_row(L, d, q, st.px, st.py, st.pz, st.vx, st.vy, st.vz, st.gx, st.gy, st.gz, nd, ndx, ndy, ndz, od, odx,
+                ody, odz);
+  STAMP_AT(env, 7);
+  A = q16_args();
+  if (A->P.auto_reset) {
+    __syncthreads();  // wave 0's decision
+    if (*reinterpret_cast<const volatile uint32_t*>(decision) != 0u) return;
+  }
+  q16_store_obs(A, L, (size_t)env * Q_N, lane);
+  STAMP_AT(env, 8);
+  STAMP_END(env, lane == 0);
+}
 
-  // ---- rewards / terminations: drone_swarm_env.py:120-172 (swarm_kernel, DYN_KIN)
-  bool pcoll;
-  if (fast) {
-    const uint32_t keep = A->P.nb_keep;
-    pcoll = __uint_as_float(nk[0] | ~keep) * FAST_HI <= A->P.thr_pair;
-    if (!pcoll && __uint_as_float(nk[0] & keep) * FAST_LO <= A->P.thr_pair) {
-      pcoll = key_zero_hit<true>(nk[0], keep, A->P.s_pair) || exact_pair_collision(L.ring, Q_N, d, px, py, pz, A->P.s_pair);
-      Q16_FLAG(2u);
-    }
+// step16q (one wave per SIMD, latency-bound) reads the kernarg segment through one pointer, so
+// the compiler batches the parameter loads at the top instead of a dependent scalar round trip at
+// each phase: 6.85 -> 6.80 us (step256 measured 46.8 -> 47.5-48.2 us that way and keeps step64's
+// per-phase re-fetch).
+// One env per 3-wave workgroup, the step's serial path split over two waves: wave 0 computes the
+// rewards, terminations, flags and state (formation-only pair pass), wave 1 the continuing env's
+// observation (keys-only pair pass, exact finish, rows), wave 2 the next episode
+// (q16_next_episode); one workgroup barrier hands wave 0's reset decision to waves 1 and 2.
+}  // namespace swarm_dev
+namespace {  // kernels: internal to this translation unit
+__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(Q16_WAVES_PER_EU)))
+swarm_step16q(const float* __restrict__ pos, const float* __restrict__ vel, const float* __restrict__ actions,
+              const uint8_t* __restrict__ active, const uint32_t* __restrict__ goal,
+              const int32_t* __restrict__ step_count, const uint8_t* __restrict__ amask, const S64Args args) {
+  (void)args;  // read through q16_args()
+  __shared__ Q16Lds ldsq[3];
+  __shared__ uint32_t decision;  // wave 0's reset decision for waves 1 and 2
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  S64ArgPtr A = q16_args();
+  const Q16Hot H{pos, vel, actions, active, goal, step_count, amask};
+  const int env = blockIdx.x;  // grid = E
+  if (wv == 2) {
+    if (A->P.auto_reset) q16_next_episode(A, env, lane, ldsq[2], &decision);
+    return;
+  }
+  Q16Lds& L = ldsq[wv];
+  const int d = lane >> 2, q = lane & 3;
+  const int M = A->P.M;
+  const size_t ea = (size_t)env * Q_N;
+  const size_t ag = ea + d;
+  if (wv == 0) {
+    STAMP_AT(env, 0);
+    STAMP_BEGIN(env, lane == 0);
+  }
+  Q16Step st;
+  Q16Raw w;
+  q16_load(A, H, env, lane, M, st, w);
+  if (wv == 0) STAMP_AT(env, 1);
+  q16_integrate(A, H, lane, M, L, st, w);
+  if (wv == 1) {
+    q16_obs_wave(A, env, lane, M, L, st, &decision);
+    return;
+  }
+  STAMP_AT(env, 2);
+  Q16_FLAGS_DECL;
+  const float px = st.px, py = st.py, pz = st.pz;
+  const bool act = st.act;
+  const int n_active = st.n_active;
+
+  // ---- formation + running-minimum pass (no keys: wave 1 ranks the observation), obstacle
+  // collisions
+  uint32_t nk[4], ok[1] = {KEY_EMPTY};  // no neighbour keys in this pass (nk unused)
+  float smin = __builtin_inff(), esum = 0.f;
+  bool ocoll = false;
+  if (st.fast) {
+    q16_pair_pass<1, true, false, true>(L.soa, d, q, px, py, pz, true, A->P.nb_keep, A->P.ds_f, nk, smin, esum);
   } else {
     Q16_FLAG(8u);
-    pcoll = smin <= A->P.thr_pair * FAST_LO;
-    if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act) {
-      pcoll = exact_pair_collision(L.ring, Q_N, d, px, py, pz, A->P.s_pair);
-      Q16_FLAG(2u);
-    }
+    q16_pair_pass<1, false, false, true>(L.soa, d, q, px, py, pz, act, A->P.nb_keep, A->P.ds_f, nk, smin, esum);
   }
-  const float curr = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
-  float rew = 0.f;
+  obstacle_pass_s64<0, true>(L.osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
+  STAMP_AT(env, 3);
+
+  // ---- terminations first (drone_swarm_env.py:120-172, swarm_kernel DYN_KIN): the pair collision
+  // from the running minimum of d~ (certain below the band, exact inside it), the goal test in
+  // squared space ((double)sqrt_rn(s) <= goal_radius exactly when s <= s_goal), so the reset
+  // decision reaches waves 1 and 2 before the reward's square root and f64 terms
+  bool pcoll = smin <= A->P.thr_pair * FAST_LO;
+  if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act) {
+    pcoll = exact_pair_collision(L.ring, Q_N, d, px, py, pz, A->P.s_pair);
+    Q16_FLAG(2u);
+  }
+  const float s_goal = sqsum_1d(st.gx - px, st.gy - py, st.gz - pz);
   bool reached = false, collided = false, term = false, trunc = false, cont = false;
   bool term_all = false, trunc_all = false;
-  int new_step = stepc;
+  int new_step = st.stepc;
   if (act) {
-    reached = (double)curr <= A->P.goal_radius;
+    reached = s_goal <= A->P.s_goal;
     collided = ocoll || pcoll;
-    double r = ((double)prev_d - (double)curr) * A->P.kp;
-    if (n_active > 1) r = r + (-A->P.kf) * ((double)esum * inv_count(n_active - 1));
-    if (reached) r = r + A->P.r_goal;
-    if (collided) r = r + A->P.r_col;
-    rew = (float)r;
   }
   const bool any_c = (__ballot(act && collided) & Q_LEAD) != 0;
   const bool any_cand = (__ballot(act && !reached && !collided) & Q_LEAD) != 0;
   if (n_active == 0) {
     term_all = true;
   } else {
-    new_step = stepc + 1;
+    new_step = st.stepc + 1;
     const bool tl = new_step >= A->P.max_steps;
     term_all = (!any_cand && !any_c && !tl) || any_c;
     trunc_all = tl && !term_all;
@@ -2967,6 +3072,25 @@ swarm_step16q(const S64Args args) {
     }
   }
   const bool do_reset = A->P.auto_reset && (term_all || trunc_all);
+
+  // ---- hand the reset decision to waves 1 (observation) and 2 (next episode)
+  if (A->P.auto_reset) {
+    if (lane == 0) decision = do_reset ? 1u : 0u;
+    __syncthreads();
+  }
+  STAMP_AT(env, 4);
+  A = q16_args();
+
+  // ---- rewards and the per-agent / per-env outputs
+  const float curr = sqrt_rn(s_goal);
+  float rew = 0.f;
+  if (act) {
+    double r = ((double)st.prev_d - (double)curr) * A->P.kp;
+    if (n_active > 1) r = r + (-A->P.kf) * ((double)esum * inv_count(n_active - 1));
+    if (reached) r = r + A->P.r_goal;
+    if (collided) r = r + A->P.r_col;
+    rew = (float)r;
+  }
   if (q == 0) {
     A->O.reward[ag] = rew;
     if (A->O.dist_goal) A->O.dist_goal[ag] = curr;
@@ -2978,14 +3102,13 @@ swarm_step16q(const S64Args args) {
     A->O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
                                    (do_reset ? SWARM_ENV_RESET : 0u));
   const uint64_t m_term = __ballot(term), m_trunc = __ballot(trunc);
-  STAMP_AT(env, 4);
 
   // ---- the terminated / truncated / active rows: three dword rows built from ballots (a resetting
   // env's drones are all active again)
   {
     const uint64_t m_act = __ballot(do_reset || cont);
     // global-typed: made opaque, a plain pointer loses its address space and the row store becomes
-    // a flat store, which every later `s_waitcnt lgkmcnt` (the obs stage) would also wait for
+    // a flat store, which every later `s_waitcnt lgkmcnt` would also wait for
     s64_gu8* p_term = (s64_gu8*)A->O.terminated;
     s64_gu8* p_trunc = (s64_gu8*)A->O.truncated;
     s64_gu8* p_act = (s64_gu8*)A->S.active;
@@ -3000,41 +3123,23 @@ swarm_step16q(const S64Args args) {
     }
   }
 
-  // ---- auto-reset: wave 1 has drawn the next episode and prepared its observation; it emits it
-  // (state, global state, obs rows) when the env resets
-  if (A->P.auto_reset) {
-    if (lane == 0) decision = do_reset ? 1u : 0u;
-    __syncthreads();
+  // ---- state write-back of a continuing env (quarter 0), env scalars (lane 0); a resetting env's
+  // new episode is wave 2's
+  if (!do_reset) {
+    if (q == 0) {
+      float* pe = A->S.pos + ag * 3;
+      float* ve = A->S.vel + ag * 3;
+      pe[0] = px; pe[1] = py; pe[2] = pz;
+      ve[0] = st.vx; ve[1] = st.vy; ve[2] = st.vz;
+    }
+    if (lane == 0) A->S.step_count[env] = new_step;
+    if (A->O.global_state && q == 0) {
+      float* gs = A->O.global_state + (size_t)env * (6 * Q_N + 3);
+      gs[3 * d] = px; gs[3 * d + 1] = py; gs[3 * d + 2] = pz;
+      gs[3 * Q_N + 3 * d] = st.vx; gs[3 * Q_N + 3 * d + 1] = st.vy; gs[3 * Q_N + 3 * d + 2] = st.vz;
+      if (d == 0) { gs[6 * Q_N + 0] = st.gx; gs[6 * Q_N + 1] = st.gy; gs[6 * Q_N + 2] = st.gz; }
+    }
   }
-  if (do_reset) return;
-  STAMP_AT(env, 5);
-
-  // ---- exact top-K: quarter q finishes neighbour slot q (q < 3) and obstacle slot q
-  float nd, ndx, ndy, ndz, od, odx, ody, odz;
-  q16_finish(A, L, d, q, M, nk, ok, true, px, py, pz, nd, ndx, ndy, ndz, od, odx, ody, odz);
-  STAMP_AT(env, 6);
-
-  // ---- state write-back (quarter 0), env scalars (lane 0)
-  if (q == 0) {
-    float* pe = A->S.pos + ag * 3;
-    float* ve = A->S.vel + ag * 3;
-    pe[0] = px; pe[1] = py; pe[2] = pz;
-    ve[0] = vx; ve[1] = vy; ve[2] = vz;
-  }
-  if (lane == 0) A->S.step_count[env] = new_step;
-  if (A->O.global_state && q == 0) {
-    float* gs = A->O.global_state + (size_t)env * (6 * Q_N + 3);
-    gs[3 * d] = px; gs[3 * d + 1] = py; gs[3 * d + 2] = pz;
-    gs[3 * Q_N + 3 * d] = vx; gs[3 * Q_N + 3 * d + 1] = vy; gs[3 * Q_N + 3 * d + 2] = vz;
-    if (d == 0) { gs[6 * Q_N + 0] = gx; gs[6 * Q_N + 1] = gy; gs[6 * Q_N + 2] = gz; }
-  }
-  STAMP_AT(env, 7);
-
-  // ---- observation rows: staged in LDS, stored as coalesced 16-B stores
-  q16_stage_row(L, d, q, px, py, pz, vx, vy, vz, gx, gy, gz, nd, ndx, ndy, ndz, od, odx, ody, odz);
-  q16_store_obs(A, L, ea, lane);
-  STAMP_AT(env, 8);
-  STAMP_END(env, lane == 0);
   Q16_FLAGS_END(env, lane);
 }
 }  // namespace
@@ -3633,6 +3738,8 @@ namespace swarm_dev {
 
 // ------------------------------------------------------------------ host side
 typedef void (*step64_fn)(const S64Args);
+typedef void (*step16q_fn)(const float*, const float*, const float*, const uint8_t*, const uint32_t*, const int32_t*,
+                           const uint8_t*, const S64Args);
 typedef void (*kernel_fn)(const KParams, const swarm_state_t, const float*, const uint8_t*, const swarm_out_t,
                           const uint8_t*, int);
 
@@ -3657,8 +3764,12 @@ kernel_fn pick_ks(int ks, int msl) {
 template <int KIND, int DYN>
 void* pick_lm(int lm, int ks, int msl) {
 #ifdef SWARM_DEV_HOT
-  // diagnostic builds (tools/): only the headline instantiation (N = 64, K = 3, Ms = 4)
-  if (lm == 2 && ks == 4 && msl == 5) return reinterpret_cast<void*>(swarm_kernel<KIND, DYN, 4, 5, 2>);
+  // diagnostic builds (tools/): only K = 3, Ms = 4 (the reset / observe of configs 2, 3 and 5)
+  if (ks == 4 && msl == 5) {
+    if (lm == 2) return reinterpret_cast<void*>(swarm_kernel<KIND, DYN, 4, 5, 2>);
+    if (lm == 1) return reinterpret_cast<void*>(swarm_kernel<KIND, DYN, 4, 5, 1>);
+    if (lm == 0) return reinterpret_cast<void*>(swarm_kernel<KIND, DYN, 4, 5, 0>);
+  }
   return nullptr;
 #else
   switch (lm) {
@@ -3949,6 +4060,11 @@ int build_kparams_uncached(const swarm_params_t* p, KParams* kp, swarm_launch_in
   k.g = (float)p->gravity;
   k.gcomp = (float)p->gravity_comp;
   k.goal_radius = p->goal_radius;
+  {  // the largest float <= goal_radius, then its squared-space threshold
+    float gr = (float)p->goal_radius;
+    if ((double)gr > p->goal_radius) gr = nextafterf(gr, -INFINITY);
+    k.s_goal = s_threshold(gr);
+  }
   k.kp = p->reward_progress_scale;
   k.r_goal = p->reward_goal;
   k.r_col = p->reward_collision;
@@ -4035,9 +4151,12 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   if (mode == MODE_STEP && step16q_applies(p, kp) && !s->env_cfg && ((uintptr_t)o->obs) % 16 == 0 &&
       ((uintptr_t)o->terminated | (uintptr_t)o->truncated | (uintptr_t)s->active) % 4 == 0) {
     const S64Args args{kp, *s, actions, amask, *o, ev};
-    // one env per 2-wave workgroup: wave 1 prepares the next episode
-    hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step16q()), dim3(kp.E), dim3(128), 0,
-                       (hipStream_t)stream, args);
+    // one env per 3-wave workgroup (rewards / observation / next episode); the first loads'
+    // addresses lead the kernel arguments (preloaded into SGPRs)
+    hipLaunchKernelGGL(reinterpret_cast<step16q_fn>(swarm_pick_step16q()), dim3(kp.E), dim3(192), 0,
+                       (hipStream_t)stream, (const float*)s->pos, (const float*)s->vel, actions,
+                       (const uint8_t*)s->active, (const uint32_t*)s->goal, (const int32_t*)s->step_count, amask,
+                       args);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SWARM_OK;
@@ -4183,10 +4302,10 @@ int swarm_query_launch(const swarm_params_t* p, swarm_launch_info_t* info) {
   const int rc = build_kparams(p, &kp, info);
   if (rc == SWARM_OK && step16q_applies(p, kp)) {  // one env per 64-lane wave, 4 lanes per drone
     info->lanes_per_env = 64;
-    info->threads_per_block = 128;  // wave 0 steps the env, wave 1 prepares its next episode
+    info->threads_per_block = 192;  // waves 0 / 1 step the env (rewards / observation), wave 2 its next episode
     info->envs_per_block = 1;
     info->blocks = kp.E;
-    info->lds_bytes = 2 * (int)sizeof(Q16Lds) + 4;
+    info->lds_bytes = 3 * (int)sizeof(Q16Lds) + 4;
     info->staged_obs = 0;
     info->kernel_id = SWARM_KERNEL_STEP16Q;
   }

@@ -85,9 +85,9 @@ def test_launch_geometry(nat, lib, n):
     assert lib.swarm_query_launch(ctypes.byref(p), ctypes.byref(info)) == 0
     lanes = 1 << (n - 1).bit_length()
     if info.kernel_id == nat.KERNEL_STEP16Q:  # config-2 specialisation: 4 lanes per drone; one env per
-        # 2-wave workgroup (wave 1 prepares the next episode)
+        # 3-wave workgroup (rewards, observation, next episode)
         assert n == 16 and info.lanes_per_env == 64 and info.staged_obs == 0
-        assert info.threads_per_block == 128 and info.envs_per_block == 1
+        assert info.threads_per_block == 192 and info.envs_per_block == 1
         assert info.blocks == 1000 and 0 < info.lds_bytes <= 160 * 1024
         return
     if info.kernel_id == nat.KERNEL_STEP256:  # config-5 specialisation: one env per 256-thread workgroup

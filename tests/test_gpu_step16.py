@@ -187,3 +187,34 @@ def test_step16q_coincident_drones_vs_oracle(dev, radius):
         assert np.abs(v.reward.cpu().numpy().astype(np.float64) - out["reward"]).max() < REWARD_TOL, f"t={t}"
         assert np.array_equal(v.terminated.cpu().numpy(), out["terminated"]), f"t={t}"
         assert np.array_equal(vec_state_numpy(v)["pos"], ns["pos"]), f"t={t}"
+
+
+@pytest.mark.parametrize("radius", [0.8, 0.5, 1.0 / 3.0])
+def test_step16q_goal_radius_boundary(dev, radius):
+    """step16q decides `reached` in squared space (s <= s_goal, the largest float s whose correctly
+    rounded root is <= goal_radius) instead of comparing sqrt_rn(s) in f64: drones placed ulp by
+    ulp across the goal radius must reach exactly as in the generic kernel."""
+    raw = dict(num_drones=16, collision_radius=0.0, goal_radius=radius, max_steps=50)
+    e = 8
+    a, b = _pair(dev, raw, e, auto_reset=False, seed=2)
+    a.reset()
+    b.reset()
+    x0 = np.float32(radius)
+    xs = [x0]
+    for _ in range(64):
+        xs.insert(0, np.nextafter(xs[0], np.float32(0)))
+        xs.append(np.nextafter(xs[-1], np.float32(10)))
+    xs = np.array(xs[: e * 16], np.float32)  # 128 consecutive floats around the radius
+    pos = np.zeros((e, 16, 3), np.float32)
+    pos[:, :, 0] = xs.reshape(e, 16)
+    obst = np.full((e, 8, 3), 9.0, np.float32)
+    obst[:, :, 1] = np.linspace(-9, 9, 8, dtype=np.float32)
+    for v in (a, b):
+        v.set_state(pos=pos, vel=np.zeros_like(pos), goal=np.zeros((e, 3), np.float32), obstacles=obst,
+                    active=np.ones((e, 16), bool), step_count=np.zeros(e, np.int32))
+    act = torch.zeros((e, 16, 3), device=dev)
+    a.step(act)
+    b.step(act)
+    _assert_same(a, b, f"goal boundary r={radius}")
+    reached = (a.info_flags.cpu().numpy() & 2) != 0
+    assert 0 < reached.sum() < reached.size  # the boundary runs through the sample

@@ -45,7 +45,7 @@ for f in range(32):
         print(f"  flags {f:2d}: waves/step {m.sum() / len(life):7.2f}  life median {np.median(life[m]):.2f}  max {life[m].max():.2f}")
 am = life.argmax(1)
 print("slowest wave per step (flags):", [int(flags[i, am[i]]) for i in range(min(20, len(am)))])
-PHASES = ["load", "integ", "pairs", "reward", "reset", "finish", "wback", "obs"]
+PHASES = ["w0load", "w0integ", "w0pass", "w0reward+writes", "w1pass-w0end", "w1finish", "w1stage", "w1wait+store"]
 ph = np.concatenate([r[3] for r in rows[5:]])
 fl = flags.reshape(-1)
 for f in sorted(set(fl.tolist())):
