@@ -1701,7 +1701,8 @@ struct S64In {
   float ox, oy, oz;                          // lanes t < M: obstacle t
   uint32_t act, has;                         // raw bytes of active / action_mask
   float damp;                                // physics: drone t's linear damping
-  uint32_t gse;  // lanes 0-2: goal x, y, z bits; lane 3: step count; lane 4: episode counter
+  uint32_t gse;  // lanes 0-2: goal x, y, z bits
+  uint32_t se;   // lane 0: step count; lane 1: episode counter
 };
 
 // The kernel's only argument.  The body re-reads the fields it needs from the kernarg segment
@@ -1740,38 +1741,72 @@ struct S64Args {
 };
 #define KARG __attribute__((address_space(4)))
 typedef const KARG S64Args* S64ArgPtr;
+// OFF: the S64Args block's byte offset in the kernarg segment (0, or behind a kernel's leading
+// preloaded arguments: S64_HOT_BYTES)
+template <uint32_t OFF = 0>
 __device__ __forceinline__ S64ArgPtr s64_args() {
-  uint64_t v = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+  uint64_t v = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr()) + OFF;
   asm volatile("" : "+s"(v));
   return reinterpret_cast<S64ArgPtr>(v);
 }
 
+// The one-wave-per-env step kernels' leading kernel arguments: the addresses of the loads the
+// integrate waits for, plus E and M, which the gfx950 kernarg preload puts in SGPRs at wave start
+// (this translation unit is built with -amdgpu-kernarg-preload-count=16; 14 user SGPRs are left
+// for it): the env bound test and those global loads need no scalar load of the kernarg segment
+// first.  The S64Args block follows them at byte offset S64_HOT_BYTES.
+struct S64Hot {
+  const float* pos;
+  const float* vel;
+  const float* actions;
+  const uint8_t* active;
+  const uint32_t* goal;
+  const uint8_t* amask;  // NULL: every agent has an action
+  int E, M;
+};
+constexpr uint32_t S64_HOT_BYTES = 56;
+static_assert(alignof(S64Args) <= 8, "S64Args at kernarg offset 56");
+
 template <int DYN = DYN_KIN>
-__device__ __forceinline__ void s64_load(S64ArgPtr A, int env, int t, S64In& c) {
-  const float* __restrict__ actions = A->actions;
-  const uint8_t* __restrict__ amask = A->amask;
-  const size_t ea = (size_t)env * S64_N;
-  const unsigned t3 = 3u * (unsigned)t;
-  const float* __restrict__ pe = A->S.pos + ea * 3;
-  const float* __restrict__ ve = A->S.vel + ea * 3;
-  const float* __restrict__ ae = actions + ea * 3;
-  {  // env-uniform words, one per lane (a uniform load would be waited for at once)
-    const uint32_t* src = t < 3 ? reinterpret_cast<const uint32_t*>(A->S.goal) + 3 * env + t
-                                : (t == 3 ? reinterpret_cast<const uint32_t*>(A->S.step_count) + env : A->S.episode + env);
-    c.gse = 0u;
-    if (t < 5) c.gse = *src;
-  }
+__device__ __forceinline__ void s64_load(S64ArgPtr A, const S64Hot& H, int env, int t, S64In& c) {
+  // 32-bit element offsets (E * 64 * 3 < 2^31, step64_applies)
+  const uint32_t ea = (uint32_t)env * S64_N;
+  const uint32_t t3 = 3u * (uint32_t)t;
+  const float* __restrict__ pe = H.pos + 3u * ea;
+  const float* __restrict__ ve = H.vel + 3u * ea;
+  const float* __restrict__ ae = H.actions + 3u * ea;
+  c.gse = 0u;
+  if (t < 3) c.gse = H.goal[3u * (uint32_t)env + (uint32_t)t];
   c.ax = ae[t3]; c.ay = ae[t3 + 1]; c.az = ae[t3 + 2];
   c.px = pe[t3]; c.py = pe[t3 + 1]; c.pz = pe[t3 + 2];
   c.vx = ve[t3]; c.vy = ve[t3 + 1]; c.vz = ve[t3 + 2];
   // unconditional loads (no phi with a default value: that would need the data at once)
-  c.act = (A->S.active + ea)[t];
-  c.has = (amask != nullptr ? amask : A->S.active)[ea + t];  // without a mask: ignored by the body
+  c.act = (H.active + ea)[t];
+  c.has = (H.amask != nullptr ? H.amask : H.active)[ea + t];  // without a mask: ignored by the body
+  // every load above is addressed from the leading (preloaded) arguments: all of them issue before
+  // the first wait for a kernarg-segment scalar load (the addresses below)
+  __builtin_amdgcn_sched_barrier(0);
+  {  // env-uniform words, one per lane (a uniform load would be waited for at once); the two bases
+    // pinned to SGPRs first (a lane-selected kernarg field became a per-lane load of the pointer)
+    // (global-typed: made opaque, a plain pointer loses its address space and the load becomes a
+    // flat load, which every later scalar-load wait would also wait for)
+    typedef const __attribute__((address_space(1))) uint32_t gcu32;
+    const gcu32* sp = (const gcu32*)A->S.step_count;
+    const gcu32* ep = (const gcu32*)A->S.episode;
+    asm volatile("" : "+s"(sp), "+s"(ep));
+    c.se = (t == 0 ? sp : ep)[env];  // every lane (branch-free): lanes > 1 re-read the episode word
+  }
   c.damp = 0.f;
   if constexpr (DYN == DYN_PHYS) c.damp = (A->S.damping + ea)[t];
-  const int m = t < A->P.M ? t : A->P.M - 1;  // lanes >= M re-load the last obstacle (unused)
-  const float* __restrict__ o = A->S.obstacles + ((size_t)env * A->P.M + m) * 3;
+  const int m = t < H.M ? t : H.M - 1;  // lanes >= M re-load the last obstacle (unused)
+  const float* __restrict__ o = A->S.obstacles + 3u * ((uint32_t)env * (uint32_t)H.M + (uint32_t)m);
   c.ox = o[0]; c.oy = o[1]; c.oz = o[2];
+  __builtin_amdgcn_sched_barrier(0);
+}
+// The leading arguments' values read from the S64Args block (kernels without preloaded arguments)
+__device__ __forceinline__ S64Hot s64_hot(S64ArgPtr A) {
+  return S64Hot{A->S.pos, A->S.vel, A->actions, A->S.active, reinterpret_cast<const uint32_t*>(A->S.goal), A->amask,
+                (int)A->P.E, A->P.M};
 }
 
 // One env of the step (all phases) from its prefetched inputs.
@@ -1780,7 +1815,7 @@ __device__ __forceinline__ void s64_load(S64ArgPtr A, int env, int t, S64In& c) 
 // LANDED: wait for them (and the queue ticket) after the pair pass, before this env issues any
 // store — vmcnt counts loads and stores in order, so a wait left to the next env's first use would
 // also wait for this env's stores.
-template <int CH, bool LANDED, class Prefetch, int DYN = DYN_KIN, bool EVAL = false>
+template <int CH, bool LANDED, class Prefetch, int DYN = DYN_KIN, bool EVAL = false, uint32_t AOFF = 0>
 __device__ __forceinline__ void s64_env(const int env, const int M, const S64In& c, float4* __restrict__ ring,
                                         float4* __restrict__ obst, float* __restrict__ stage, const int lane,
                                         Prefetch&& prefetch) {
@@ -1794,7 +1829,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   const unsigned t3 = 3u * (unsigned)t;
   const size_t ea = (size_t)env * S64_N;  // first agent of the env (uniform)
   float* __restrict__ const soa = reinterpret_cast<float*>(ring + S64_N);  // S64Lds::w.soa
-  S64ArgPtr A = s64_args();  // re-fetched at every phase boundary
+  S64ArgPtr A = s64_args<AOFF>();  // re-fetched at every phase boundary
   STAMP_VAR(const int srec = env + (int)A->P.env_offset);  // stamp record: the global env (env groups)
   STAMP_AT(srec, 0);
   STAMP_BEGIN(srec, (threadIdx.x & 63) == 0);
@@ -1803,15 +1838,16 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   float gx = __uint_as_float(__builtin_amdgcn_readlane(c.gse, 0));
   float gy = __uint_as_float(__builtin_amdgcn_readlane(c.gse, 1));
   float gz = __uint_as_float(__builtin_amdgcn_readlane(c.gse, 2));
-  const int stepc = (int)__builtin_amdgcn_readlane(c.gse, 3);
-  const uint32_t episode0 = (uint32_t)__builtin_amdgcn_readlane(c.gse, 4);
   float ax = c.ax, ay = c.ay, az = c.az;
-  const bool has = s64_args()->amask == nullptr || c.has != 0;
+  uint32_t hraw = c.has;
+  // pinned here: left to the compiler, the action / mask loads sank into the `act` branch of the
+  // integrate and issued only after every earlier load had returned (a second round trip)
+  asm volatile("" : "+v"(ax), "+v"(ay), "+v"(az), "+v"(hraw));
+  const bool has = s64_args<AOFF>()->amask == nullptr || hraw != 0;
   float px = c.px, py = c.py, pz = c.pz;
   float vx = c.vx, vy = c.vy, vz = c.vz;
   bool act = c.act != 0;
   float* __restrict__ const osoa = reinterpret_cast<float*>(obst + S64_MMAX);  // S64Lds::w.osoa
-  if (t < M) s64_put_obst(obst, osoa, t, c.ox, c.oy, c.oz);
   const int n_active = __popcll(__ballot(act));
   STAMP_AT(srec, 1);
 
@@ -1883,12 +1919,17 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     py = clampf(py, A->P.neg_half_w, A->P.half_w);
     pz = clampf(pz, A->P.neg_half_w, A->P.half_w);
   }
+  // obstacles to LDS and the step / episode words here, after the integrate: their loads
+  // (addressed from the kernarg segment, issued last) land while it runs
+  if (t < M) s64_put_obst(obst, osoa, t, c.ox, c.oy, c.oz);
+  const int stepc = (int)__builtin_amdgcn_readlane(c.se, 0);
+  const uint32_t episode0 = (uint32_t)__builtin_amdgcn_readlane(c.se, 1);
   // eligibility: active drones (kinematic), every drone (physics contacts)
   s64_put(ring, soa, t, px, py, pz, (DYN == DYN_PHYS || act) ? 1.f : 0.f);
   wave_sync();
   prefetch();  // `c` is dead from here on
   STAMP_AT(srec, 2);
-  A = s64_args();
+  A = s64_args<AOFF>();
 
   // ---- pair + obstacle passes
   uint32_t nk[KS], ok[MSL];
@@ -1910,7 +1951,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     // without neighbour keys (they would rank the positions the reset replaces): formation terms
     // and the running minimum only, the same sums bit for bit
     obstacle_pass_s64<MSL, true>(osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
-    A = s64_args();
+    A = s64_args<AOFF>();
     early = fast && A->P.auto_reset &&
             (__ballot(act && ocoll) != 0 || stepc + 1 >= A->P.max_steps);
     if (early) {
@@ -1922,7 +1963,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   }
   if constexpr (LANDED) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the next env's inputs are in
   STAMP_AT(srec, 3);
-  A = s64_args();
+  A = s64_args<AOFF>();
 
   // ---- exact top-K (finish_keys, rare exact_select)
   float wd[KS], od[MSL];
@@ -2191,7 +2232,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   }
   if constexpr (EVAL) __builtin_amdgcn_sched_barrier(0);
   STAMP_AT(srec, 5);
-  A = s64_args();
+  A = s64_args<AOFF>();
 
   // ---- in-kernel auto-reset (wave-uniform): new episode, then its key passes
   uint32_t episode_new = episode0;
@@ -2239,7 +2280,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   select_topk(DYN == DYN_KIN && !do_reset);
 
   STAMP_AT(srec, 6);
-  A = s64_args();
+  A = s64_args<AOFF>();
   // ---- state write-back
   const bool new_act = do_reset || (DYN == DYN_PHYS ? (act && !(term_all || trunc_all)) : cont);
   float* __restrict__ posE = A->S.pos + ea * 3;
@@ -2295,7 +2336,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
   }
 
   STAMP_AT(srec, 7);
-  A = s64_args();
+  A = s64_args<AOFF>();
   // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)] (drone_swarm_env.py:226-291)
   float row[D];
   row[0] = px; row[1] = py; row[2] = pz;
@@ -2372,24 +2413,30 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
 [[maybe_unused]] constexpr int S64_WG_ENVS = S64_WG_ENVS_C;
 // The body of both one-wave-per-env kernels (kinematic / physics).
 template <int CH, int G, int DYN, bool EVAL = false>
-__device__ __forceinline__ void s64_once_body() {
+__device__ __forceinline__ void s64_once_body(const S64Hot& H) {
   __shared__ S64Lds<CH> lds[G];
   const int t = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int env = blockIdx.x * G + w;
-  if (env >= s64_args()->P.E) return;  // whole wave (the last workgroup of a ragged E)
+  if (env >= H.E) return;  // whole wave (the last workgroup of a ragged E)
   S64In cur;
-  s64_load<DYN>(s64_args(), env, t, cur);
-  s64_env<CH, false, void (*)(), DYN, EVAL>(env, s64_args()->P.M, cur, lds[w].w.ring, lds[w].w.obst,
-                                      reinterpret_cast<float*>(lds[w].stage), t, []() {});
+  s64_load<DYN>(s64_args<S64_HOT_BYTES>(), H, env, t, cur);
+  s64_env<CH, false, void (*)(), DYN, EVAL, S64_HOT_BYTES>(env, H.M, cur, lds[w].w.ring, lds[w].w.obst,
+                                                         reinterpret_cast<float*>(lds[w].stage), t, []() {});
 }
+// The once-kernels' leading arguments (S64Hot's fields, preloaded) and the S64Args block
+#define S64_ONCE_PARAMS                                                                                          \
+  const float *__restrict__ pos, const float *__restrict__ vel, const float *__restrict__ actions,              \
+      const uint8_t *__restrict__ active, const uint32_t *__restrict__ goal, const uint8_t *__restrict__ amask, \
+      int E, int M, const S64Args args
+#define S64_ONCE_HOT S64Hot{pos, vel, actions, active, goal, amask, E, M}
 }  // namespace swarm_dev
 namespace {  // kernels: internal to this translation unit
 template <int CH, int G>
 __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(8)))
-swarm_step64_once(const S64Args args) {
-  (void)args;  // read through s64_args()
-  s64_once_body<CH, G, DYN_KIN>();
+swarm_step64_once(S64_ONCE_PARAMS) {
+  (void)args;  // read through s64_args<S64_HOT_BYTES>()
+  s64_once_body<CH, G, DYN_KIN>(S64_ONCE_HOT);
 }
 }  // namespace
 namespace swarm_dev {
@@ -2403,15 +2450,15 @@ namespace swarm_dev {
 namespace {  // kernels: internal to this translation unit
 template <int CH, int G>
 __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(S64_EVAL_WAVES)))
-swarm_step64_eval_once(const S64Args args) {
+swarm_step64_eval_once(S64_ONCE_PARAMS) {
   (void)args;
-  s64_once_body<CH, G, DYN_KIN, true>();
+  s64_once_body<CH, G, DYN_KIN, true>(S64_ONCE_HOT);
 }
 template <int CH, int G>
 __global__ void __launch_bounds__(64 * G) __attribute__((amdgpu_waves_per_eu(8)))
-swarm_step64_phys_once(const S64Args args) {
+swarm_step64_phys_once(S64_ONCE_PARAMS) {
   (void)args;
-  s64_once_body<CH, G, DYN_PHYS>();
+  s64_once_body<CH, G, DYN_PHYS>(S64_ONCE_HOT);
 }
 }  // namespace
 namespace swarm_dev {
@@ -2460,7 +2507,7 @@ swarm_step64(const S64Args args) {
   };
   S64In cur;
   const bool first = env >= 0;
-  if (first) s64_load(A, env, t, cur);
+  if (first) s64_load(A, s64_hot(A), env, t, cur);
   uint32_t ticket = draw();
   // the first env's inputs and ticket land here, so that no path into the loop header carries a
   // pending load (the in-loop ones are waited for mid-body, before any store): the header then
@@ -2470,7 +2517,7 @@ swarm_step64(const S64Args args) {
     const int nxt = settle(ticket);
     s64_env<CH, true>(env, M, cur, ring, obst, stage, t, [&]() {
       if (nxt >= 0) {
-        s64_load(s64_args(), nxt, t, cur);
+        s64_load(s64_args(), s64_hot(s64_args()), nxt, t, cur);
         ticket = draw();
       }
     });
@@ -3738,6 +3785,8 @@ namespace swarm_dev {
 
 // ------------------------------------------------------------------ host side
 typedef void (*step64_fn)(const S64Args);
+typedef void (*step64o_fn)(const float*, const float*, const float*, const uint8_t*, const uint32_t*, const uint8_t*, int,
+                           int, const S64Args);
 typedef void (*step16q_fn)(const float*, const float*, const float*, const uint8_t*, const uint32_t*, const int32_t*,
                            const uint8_t*, const S64Args);
 typedef void (*kernel_fn)(const KParams, const swarm_state_t, const float*, const uint8_t*, const swarm_out_t,
@@ -4140,10 +4189,11 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
     if (st.work)
       hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step64(true, false)), dim3(grid), dim3(64), 0,
                          (hipStream_t)stream, args);
-    else
-      hipLaunchKernelGGL(reinterpret_cast<step64_fn>(ev.status ? swarm_pick_step64_eval() : swarm_pick_step64(false, phys)),
+    else  // the first loads' addresses, E and M lead the arguments (preloaded into SGPRs)
+      hipLaunchKernelGGL(reinterpret_cast<step64o_fn>(ev.status ? swarm_pick_step64_eval() : swarm_pick_step64(false, phys)),
                          dim3((kp.E + S64_WG_ENVS - 1) / S64_WG_ENVS), dim3(64 * S64_WG_ENVS), 0, (hipStream_t)stream,
-                         args);
+                         (const float*)st.pos, (const float*)st.vel, actions, (const uint8_t*)st.active,
+                         (const uint32_t*)st.goal, amask, kp.E, kp.M, args);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SWARM_OK;
