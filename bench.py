@@ -66,7 +66,9 @@ MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3, "f32x3": 2500.0 / 3}
 PRESETS = {
     "headline": dict(drones=64, envs=8192, ctde=False, groups=3, groups_graph=4,
                      label="config 3: N=64 x E=8192 on 1 MI355X (headline); config 4 per GPU"),
-    "n16": dict(drones=16, envs=1024, ctde=False,
+    # config 2 times eager launches at every K: its 5.5 us kernel is shorter than a replayed graph
+    # node's dispatch gap (5.50-5.57 eager vs 5.85-5.86 us graph at K = 500 / 1000, r05u)
+    "n16": dict(drones=16, envs=1024, ctde=False, graph=False,
                 label="config 2: N=16 x E=1024 on 1 MI355X (launch-latency-bound)"),
     "n256": dict(drones=256, envs=1024, ctde=True, groups=2, groups_graph=4,
                  label="config 5 per-GPU slab: N=256 x E=1024 with CTDE global_state"),
@@ -153,6 +155,8 @@ def parse(argv=None):
     a.envs = pre["envs"] if a.envs is None else a.envs
     a.ctde = pre["ctde"] if a.ctde is None else a.ctde
     a.label = pre["label"]
+    if not pre.get("graph", True):
+        a.no_graph = True
     a.groups_explicit = a.groups is not None
     if a.groups is None:
         # 4 groups where the timed region replays graphs (K > 256, no CTDE gather): 25.2 vs
