@@ -1769,7 +1769,7 @@ static_assert(alignof(S64Args) <= 8, "S64Args at kernarg offset 56");
 
 template <int DYN = DYN_KIN>
 __device__ __forceinline__ void s64_load(S64ArgPtr A, const S64Hot& H, int env, int t, S64In& c) {
-  // 32-bit element offsets (E * 64 * 3 < 2^31, step64_applies)
+  // 32-bit element offsets (E <= SPEC_MAX_E = 2^22, step64_applies: E x 64 x 3 < 2^32)
   const uint32_t ea = (uint32_t)env * S64_N;
   const uint32_t t3 = 3u * (uint32_t)t;
   const float* __restrict__ pe = H.pos + 3u * ea;
@@ -2896,7 +2896,7 @@ struct Q16Raw {
 // Loads (the four lanes of a drone read the same words).
 __device__ __forceinline__ void q16_load(S64ArgPtr A, const Q16Hot& H, int env, int lane, int M, Q16Step& st,
                                          Q16Raw& w) {
-  // 32-bit element offsets (E * 16 * 37 < 2^31, step16q_applies): 64-bit index arithmetic let the
+  // 32-bit element offsets (E <= SPEC_MAX_E, step16q_applies): 64-bit index arithmetic let the
   // register allocator tie an address's unused high half to the goal word's load register, a false
   // dependency that made every later load wait for that one
   const uint32_t ag = (uint32_t)env * Q_N + (uint32_t)(lane >> 2), ag3 = 3u * ag;
@@ -3933,15 +3933,18 @@ int obs_dim_of(const swarm_params_t* p) {
 
 // The headline specialisation swarm_step64 covers N = 64, K = 3, Ms = 4, 4 <= M <= 16 in
 // kinematic/swarm mode (buffer alignment is checked at launch).
+// The specialisations' loads index with 32-bit element offsets (E x N x 3 and E x M x 3 < 2^32):
+// batches above 2^22 envs take the generic kernel.
+constexpr int SPEC_MAX_E = 1 << 22;
 bool step64_applies(const swarm_params_t* p, const KParams& k) {
   return p->kernel_path == SWARM_PATH_AUTO && k.N == S64_N && k.K == S64_K && k.Ms == S64_MS && k.M >= S64_MS &&
-         k.M <= S64_MMAX && (p->dynamics == DYN_KIN || p->dynamics == DYN_PHYS);
+         k.M <= S64_MMAX && k.E <= SPEC_MAX_E && (p->dynamics == DYN_KIN || p->dynamics == DYN_PHYS);
 }
 
 // The config-2 specialisation swarm_step16q covers N = 16, K = 3, Ms = 4, 4 <= M <= 16, kinematic.
 bool step16q_applies(const swarm_params_t* p, const KParams& k) {
   return p->kernel_path == SWARM_PATH_AUTO && k.N == Q_N && k.K == Q_K && k.Ms == Q_MS && k.M >= Q_MS &&
-         k.M <= Q_MMAX && p->dynamics == DYN_KIN;
+         k.M <= Q_MMAX && k.E <= SPEC_MAX_E && p->dynamics == DYN_KIN;
 }
 
 // The config-5 specialisation swarm_step256 covers N = 256, K = 3, Ms = 4, 4 <= M <= 16, kinematic.
