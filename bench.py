@@ -99,6 +99,8 @@ def parse(argv=None):
                     help="one workgroup per env instead of the persistent env queue")
     ap.add_argument("--no-graph", action="store_true",
                     help="time the whole-job rate with eager launches instead of hipGraph replay")
+    ap.add_argument("--use-graph", action="store_true",
+                    help="hipGraph replay for K > 256 even where the preset times eager launches (n16)")
     ap.add_argument("--ctde", action="store_true", default=None,
                     help="also emit global_state and all-gather it (config 5)")
     ap.add_argument("--no-ctde", dest="ctde", action="store_false",
@@ -155,7 +157,7 @@ def parse(argv=None):
     a.envs = pre["envs"] if a.envs is None else a.envs
     a.ctde = pre["ctde"] if a.ctde is None else a.ctde
     a.label = pre["label"]
-    if not pre.get("graph", True):
+    if not pre.get("graph", True) and not a.use_graph:
         a.no_graph = True
     a.groups_explicit = a.groups is not None
     if a.groups is None:
