@@ -66,9 +66,10 @@ MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3, "f32x3": 2500.0 / 3}
 PRESETS = {
     "headline": dict(drones=64, envs=8192, ctde=False, groups=3, groups_graph=4,
                      label="config 3: N=64 x E=8192 on 1 MI355X (headline); config 4 per GPU"),
-    # config 2 times eager launches at every K: its 5.5 us kernel is shorter than a replayed graph
-    # node's dispatch gap (5.50-5.57 eager vs 5.85-5.86 us graph at K = 500 / 1000, r05u)
-    "n16": dict(drones=16, envs=1024, ctde=False, graph=False,
+    # config 2 keeps graph replay for K > 256: 5.74-5.86 us per step on four boxes, while eager
+    # launches of its 5.5 us kernel are bound by the host's launch rate, 5.47-6.84 us box to box
+    # (profiles/r05u, r05x, r05y, r05z)
+    "n16": dict(drones=16, envs=1024, ctde=False,
                 label="config 2: N=16 x E=1024 on 1 MI355X (launch-latency-bound)"),
     "n256": dict(drones=256, envs=1024, ctde=True, groups=2, groups_graph=4,
                  label="config 5 per-GPU slab: N=256 x E=1024 with CTDE global_state"),
