@@ -3043,6 +3043,9 @@ swarm_step16q(const float* __restrict__ pos, const float* __restrict__ vel, cons
   S64ArgPtr A = q16_args();
   const Q16Hot H{pos, vel, actions, active, goal, step_count, amask};
   const int env = blockIdx.x;  // grid = E
+  // the step's waves (the launch's critical path) issue ahead of the next-episode waves sharing
+  // their SIMDs: 5.82-5.84 -> 5.71-5.73 us per step (priority 3 no better, r05aa)
+  if (wv != 2) __builtin_amdgcn_s_setprio(1);
   if (wv == 2) {
     if (A->P.auto_reset) q16_next_episode(A, env, lane, ldsq[2], &decision);
     return;
