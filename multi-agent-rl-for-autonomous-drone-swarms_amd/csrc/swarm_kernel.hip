@@ -3242,7 +3242,34 @@ struct H256Lds {
   } x;
 };
 
-__device__ __forceinline__ void h_put(H256Lds& L, int w, int t, float x, float y, float z, float el) {
+// step256 on a 512-thread workgroup (SWARM_S256_WIDE): waves 0-3 (primary) and 4-7 (secondary)
+// both hold drones 64b .. 64b + 63 of block b = wave & 3.  The primary evaluates blocks (b, b) and
+// half of (b, b + 2), the secondary all of (b, b + 1): 64 rotations each instead of 128.  The
+// secondary's own-side results come to the primary through LDS as the mirrors do.  Plane layout:
+// per block and plane (x, y, z, eligibility) two copies of the 128-entry wrap segment, copy 0 at
+// dword 0 and copy 1 shifted by one dword at H_C1 + 1 (H_C1 = 30 mod 64 apart: a ds_read_b64
+// half-wave's two copies land on disjoint banks), so each lane reads aligned rotation pairs.
+constexpr int H_C1 = 158;
+constexpr int H_PS = 288;  // dwords per plane: copy 0 [0, 128), copy 1 [H_C1 + 1, H_C1 + 129)
+struct H256WLds {
+  float seg2[4][4][H_PS];
+  float4 ring[H_N];
+  float4 obst[H_MMAX];
+  float osoa[3 * H_MMAX];
+  float4 goal;
+  uint32_t red[4];
+  union {
+    struct {
+      double dsum[H_N];          // the secondary's own formation sums
+      float sum[2][H_N];         // mirror sums: [0] from block (b - 1, b), [1] from (b - 2, b)
+      float mn[3][H_N];          // mirror minima [0], [1]; the secondary's own minima [2]
+    } p1;
+    uint32_t keys[3][4][H_N];  // mirror lists [0] (b - 1, b), [1] (b - 2, b); the secondary's own [2]
+  } x;
+};
+
+template <class LT>
+__device__ __forceinline__ void h_put(LT& L, int w, int t, float x, float y, float z, float el) {
   L.seg[w][0][t] = x; L.seg[w][0][t + 64] = x;
   L.seg[w][1][t] = y; L.seg[w][1][t + 64] = y;
   L.seg[w][2][t] = z; L.seg[w][2][t + 64] = z;
@@ -3258,7 +3285,8 @@ __device__ __forceinline__ void h_bases_p(float (*seg)[NP][H_BL], int b, int t, 
   P1 = (s64_lds_cf*)&seg[b][2][t];
   asm volatile("" : "+v"(P0), "+v"(P1));
 }
-__device__ __forceinline__ void h_bases(H256Lds& L, int b, int t, s64_lds_cf*& P0, s64_lds_cf*& P1) {
+template <class LT>
+__device__ __forceinline__ void h_bases(LT& L, int b, int t, s64_lds_cf*& P0, s64_lds_cf*& P1) {
   h_bases_p<4>(L.seg, b, t, P0, P1);
 }
 // Traveling minima are kept as float bits and reduced with v_min_u32 (every value is a
@@ -3270,11 +3298,29 @@ __device__ __forceinline__ uint32_t wave_ror1_u(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x13C, 0xF, 0xF, true);
 }
 
+// Plane reads of the wide kernel's two-copy layout (H256WLds::seg2, PS dwords per plane): lane t's
+// base addresses copy (t + PAR) & 1, in which the rotation pair (r - 1, r) of every r with
+// r - 1 = PAR (mod 2) is 8-B aligned, so the pair is one ds_read_b64 (2 LDS cycles) instead of a
+// ds_read2_b32 (4)
+typedef const __attribute__((address_space(3))) s64_f2 s64_lds_cf2;
+template <int PS>
+__device__ __forceinline__ s64_f2 hw_ld2(s64_lds_cf* P, int plane, int r) {  // {X[r], X[r - 1]}
+  const s64_f2 v = *(volatile s64_lds_cf2*)(P + plane * PS + r - 1);
+  return v.yx;
+}
+template <int PS, int PAR>
+__device__ __forceinline__ float hw_ld1(s64_lds_cf* P, int plane, int r) {  // X[r] from its aligned pair
+  const int lo = (((r - 1) & 1) == PAR) ? r - 1 : r;
+  const s64_f2 v = *(volatile s64_lds_cf2*)(P + plane * PS + lo);
+  return lo == r ? v.x : v.y;
+}
+
 // Formation + minimum pass over rotations RHI, RHI - 1, .., RLO of one block (X/Y/Z/E = the
 // block's plane segments at lane t).  Own side: formation partial sum `esum` (flushed into the
 // f64 `fsum` every 8 rotations) and minimum `mn` of d~ = v_sqrt_f32(s') over eligible pairs.
 // TRAVEL: the pair's value also enters the traveling sum / minimum (the partner's side).
-template <bool FAST, int RHI, int RLO, bool TRAVEL>
+// PS > 0: the two-copy layout (hw_ld2 / hw_ld1 from the base P0; P1 unused).
+template <bool FAST, int RHI, int RLO, bool TRAVEL, int PS = 0, int PAR = 0>
 __device__ __forceinline__ void h_seg1(s64_lds_cf* __restrict__ P0, s64_lds_cf* __restrict__ P1, bool self,
                                        float px, float py, float pz, float ds, double& fsum, float& mn, float& tsum,
                                        uint32_t& tmin) {
@@ -3282,6 +3328,7 @@ __device__ __forceinline__ void h_seg1(s64_lds_cf* __restrict__ P0, s64_lds_cf* 
   s64_lds_cf* Y = P0 + H_BL;
   s64_lds_cf* Z = P1;
   s64_lds_cf* E = P1 + H_BL;
+  static_assert(PS == 0 || RHI == RLO || ((RHI - 1) & 1) == PAR, "rotation pairs off the copy's alignment");
   float esum = 0.f;
   const float selff = self ? 1.f : 0.f;
 #pragma unroll
@@ -3289,7 +3336,12 @@ __device__ __forceinline__ void h_seg1(s64_lds_cf* __restrict__ P0, s64_lds_cf* 
     const bool two = r - 1 >= RLO;
     float d[2];
     if (two) {
-      const s64_f2 XX = {X[r], X[r - 1]}, YY = {Y[r], Y[r - 1]}, ZZ = {Z[r], Z[r - 1]};
+      s64_f2 XX, YY, ZZ;
+      if constexpr (PS > 0) {
+        XX = hw_ld2<PS>(P0, 0, r); YY = hw_ld2<PS>(P0, 1, r); ZZ = hw_ld2<PS>(P0, 2, r);
+      } else {
+        XX = s64_f2{X[r], X[r - 1]}; YY = s64_f2{Y[r], Y[r - 1]}; ZZ = s64_f2{Z[r], Z[r - 1]};
+      }
       const s64_f2 dx = XX - px, dy = YY - py, dz = ZZ - pz;
       s64_f2 s = dx * dx;
       s = __builtin_elementwise_fma(dy, dy, s);
@@ -3297,7 +3349,11 @@ __device__ __forceinline__ void h_seg1(s64_lds_cf* __restrict__ P0, s64_lds_cf* 
       d[0] = __builtin_amdgcn_sqrtf(s.x);
       d[1] = __builtin_amdgcn_sqrtf(s.y);
     } else {
-      d[0] = __builtin_amdgcn_sqrtf(sqsum_rank(X[r] - px, Y[r] - py, Z[r] - pz));
+      if constexpr (PS > 0)
+        d[0] = __builtin_amdgcn_sqrtf(sqsum_rank(hw_ld1<PS, PAR>(P0, 0, r) - px, hw_ld1<PS, PAR>(P0, 1, r) - py,
+                                                 hw_ld1<PS, PAR>(P0, 2, r) - pz));
+      else
+        d[0] = __builtin_amdgcn_sqrtf(sqsum_rank(X[r] - px, Y[r] - py, Z[r] - pz));
       d[1] = 0.f;
     }
     float term[2];
@@ -3319,7 +3375,10 @@ __device__ __forceinline__ void h_seg1(s64_lds_cf* __restrict__ P0, s64_lds_cf* 
       // 3e38 (above every threshold) instead of inf
       float tv = term[h], dv = d[h];
       if constexpr (!FAST) {
-        const float ef = selff * E[rr];
+        float er;
+        if constexpr (PS > 0) er = hw_ld1<PS, PAR>(P0, 3, rr);
+        else er = E[rr];
+        const float ef = selff * er;
         tv = tv * ef;
         dv = fmaxf(dv, (1.f - ef) * 3e38f);
       }
@@ -3344,7 +3403,7 @@ __device__ __forceinline__ void h_seg1(s64_lds_cf* __restrict__ P0, s64_lds_cf* 
 // Keys pass (s' keys) over rotations RHI .. RLO of one block: own keys into `nk` with partner
 // code CO + r; MIRROR: the pair value goes by ds_bpermute to lane t + r, whose target list `mk`
 // takes it with code CM + (64 - r) % 64 (lane offset back to this lane, block delta in CM).
-template <int RHI, int RLO, int CO, int CM, bool MIRROR>
+template <int RHI, int RLO, int CO, int CM, bool MIRROR, int PS = 0, int PAR = 0>
 __device__ __forceinline__ void h_seg0(s64_lds_cf* __restrict__ P0, s64_lds_cf* __restrict__ P1, uint32_t t4, float px,
                                        float py, float pz, uint32_t keep, uint32_t (&nk)[4], uint32_t (&mk)[4]) {
   s64_lds_cf* X = P0;
@@ -3352,6 +3411,7 @@ __device__ __forceinline__ void h_seg0(s64_lds_cf* __restrict__ P0, s64_lds_cf* 
   s64_lds_cf* Z = P1;
   // keep in a VGPR: (value & keep) | code is then one v_and_or_b32 with the code from an SGPR
   // (a VOP3 literal is not encodable on gfx9)
+  static_assert(PS == 0 || RHI == RLO || ((RHI - 1) & 1) == PAR, "rotation pairs off the copy's alignment");
   uint32_t keepv = keep;
   asm volatile("" : "+v"(keepv));
 #pragma unroll
@@ -3359,7 +3419,12 @@ __device__ __forceinline__ void h_seg0(s64_lds_cf* __restrict__ P0, s64_lds_cf* 
     const bool two = r - 1 >= RLO;
     float s[2];
     if (two) {
-      const s64_f2 XX = {X[r], X[r - 1]}, YY = {Y[r], Y[r - 1]}, ZZ = {Z[r], Z[r - 1]};
+      s64_f2 XX, YY, ZZ;
+      if constexpr (PS > 0) {
+        XX = hw_ld2<PS>(P0, 0, r); YY = hw_ld2<PS>(P0, 1, r); ZZ = hw_ld2<PS>(P0, 2, r);
+      } else {
+        XX = s64_f2{X[r], X[r - 1]}; YY = s64_f2{Y[r], Y[r - 1]}; ZZ = s64_f2{Z[r], Z[r - 1]};
+      }
       const s64_f2 dx = XX - px, dy = YY - py, dz = ZZ - pz;
       s64_f2 q = dx * dx;
       q = __builtin_elementwise_fma(dy, dy, q);
@@ -3367,7 +3432,10 @@ __device__ __forceinline__ void h_seg0(s64_lds_cf* __restrict__ P0, s64_lds_cf* 
       s[0] = q.x;
       s[1] = q.y;
     } else {
-      s[0] = sqsum_rank(X[r] - px, Y[r] - py, Z[r] - pz);
+      if constexpr (PS > 0)
+        s[0] = sqsum_rank(hw_ld1<PS, PAR>(P0, 0, r) - px, hw_ld1<PS, PAR>(P0, 1, r) - py, hw_ld1<PS, PAR>(P0, 2, r) - pz);
+      else
+        s[0] = sqsum_rank(X[r] - px, Y[r] - py, Z[r] - pz);
       s[1] = 0.f;
     }
     // the own key goes to the mirror as is; the mirror swaps its code CO + r for CM + (64 - r) % 64
@@ -3463,6 +3531,90 @@ __device__ __forceinline__ void h_pass0(H256Lds& L, int w, int t, float px, floa
   for (int s = 0; s < 4; ++s) {
     L.x.keys[0][s][64 * b1 + t] = kb[s];
     L.x.keys[1][s][64 * b2 + t] = kc[s];
+  }
+}
+
+__device__ __forceinline__ void hw_put(H256WLds& L, int w, int t, float x, float y, float z, float el) {
+  const float v[4] = {x, y, z, el};
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    L.seg2[w][p][t] = v[p]; L.seg2[w][p][t + 64] = v[p];
+    L.seg2[w][p][H_C1 + 1 + t] = v[p]; L.seg2[w][p][H_C1 + 65 + t] = v[p];
+  }
+  L.ring[64 * w + t] = make_float4(x, y, z, el);
+}
+// Lane t's base into block b's planes for rotation pairs (r - 1, r) with r - 1 = PAR (mod 2)
+template <int PAR>
+__device__ __forceinline__ s64_lds_cf* hw_base(H256WLds& L, int b, int t) {
+  const int c = (t + PAR) & 1;
+  s64_lds_cf* P = (s64_lds_cf*)&L.seg2[b][0][(c ? H_C1 + 1 : 0) + t];
+  asm volatile("" : "+v"(P));
+  return P;
+}
+
+// The wide kernel's halves of h_pass1 / h_pass0.  Primary: block (w, w) and half of (w, w + 2);
+// secondary: block (w, w + 1), its own side into fsum / smin / nk, the mirror into set [0].
+template <bool FAST, bool PRIMARY>
+__device__ __forceinline__ void hw_pass1(H256WLds& L, int w, int t, bool self, float px, float py, float pz, float ds,
+                                         double& fsum, float& smin) {
+  const int b1 = (w + 1) & 3, b2 = (w + 2) & 3;
+  s64_lds_cf* const none = nullptr;
+  if constexpr (PRIMARY) {
+    s64_lds_cf* P0 = hw_base<0>(L, w, t);
+    float ta = 0.f, dummy = 0.f;
+    uint32_t tam = 0x7f800000u, dummym = 0x7f800000u;
+    h_seg1<FAST, 31, 1, true, H_PS, 0>(P0, none, self, px, py, pz, ds, fsum, smin, ta, tam);
+    fsum += (double)wave_ror1(ta);
+    smin = fminf(smin, __uint_as_float(wave_ror1_u(tam)));
+    h_seg1<FAST, 32, 32, false, H_PS, 0>(P0, none, self, px, py, pz, ds, fsum, smin, dummy, dummym);
+    float tc = 0.f;
+    uint32_t tcm = 0x7f800000u;
+    if (w < 2) {
+      h_seg1<FAST, 31, 0, true, H_PS, 0>(hw_base<0>(L, b2, t), none, self, px, py, pz, ds, fsum, smin, tc, tcm);
+    } else {
+      h_seg1<FAST, 32, 1, true, H_PS, 1>(hw_base<1>(L, b2, t), none, self, px, py, pz, ds, fsum, smin, tc, tcm);
+      tc = wave_ror1(tc);
+      tcm = wave_ror1_u(tcm);
+    }
+    L.x.p1.sum[1][64 * b2 + t] = tc;
+    L.x.p1.mn[1][64 * b2 + t] = __uint_as_float(tcm);
+  } else {
+    float tb = 0.f;
+    uint32_t tbm = 0x7f800000u;
+    h_seg1<FAST, 63, 0, true, H_PS, 0>(hw_base<0>(L, b1, t), none, self, px, py, pz, ds, fsum, smin, tb, tbm);
+    L.x.p1.sum[0][64 * b1 + t] = tb;
+    L.x.p1.mn[0][64 * b1 + t] = __uint_as_float(tbm);
+    L.x.p1.dsum[64 * w + t] = fsum;
+    L.x.p1.mn[2][64 * w + t] = smin;
+  }
+}
+
+template <bool PRIMARY>
+__device__ __forceinline__ void hw_pass0(H256WLds& L, int w, int t, float px, float py, float pz, uint32_t keep,
+                                         uint32_t (&nk)[4]) {
+  const int b1 = (w + 1) & 3, b2 = (w + 2) & 3;
+  const uint32_t t4 = (uint32_t)t << 2;
+  uint32_t km[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) km[s] = KEY_EMPTY;
+  s64_lds_cf* const none = nullptr;
+  if constexpr (PRIMARY) {
+    s64_lds_cf* P0 = hw_base<0>(L, w, t);
+    h_seg0<31, 1, 0, 0, true, H_PS, 0>(P0, none, t4, px, py, pz, keep, nk, nk);
+    h_seg0<32, 32, 0, 0, false, H_PS, 0>(P0, none, t4, px, py, pz, keep, nk, nk);
+    if (w < 2)
+      h_seg0<31, 0, 128, 128, true, H_PS, 0>(hw_base<0>(L, b2, t), none, t4, px, py, pz, keep, nk, km);
+    else
+      h_seg0<32, 1, 128, 128, true, H_PS, 1>(hw_base<1>(L, b2, t), none, t4, px, py, pz, keep, nk, km);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) L.x.keys[1][s][64 * b2 + t] = km[s];
+  } else {
+    h_seg0<63, 0, 64, 192, true, H_PS, 0>(hw_base<0>(L, b1, t), none, t4, px, py, pz, keep, nk, km);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      L.x.keys[0][s][64 * b1 + t] = km[s];
+      L.x.keys[2][s][64 * w + t] = nk[s];
+    }
   }
 }
 
@@ -3781,6 +3933,303 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   STAMP256(8);
   STAMP_END(env, i == 0);
 }
+
+// The same step on 512 threads (H256WLds): the primary wave of block b runs every phase of
+// swarm_step256 for drones 64b .. 64b + 63 except block (b, b + 1) of both pair passes, which
+// its secondary wave (b + 4) evaluates at the same time; the secondary also loads, draws and
+// writes the obstacles and draws the goal.  Results as swarm_step256's (formation sums in
+// another order: rewards within 1e-5).
+#ifndef SWARM_S256W_WAVES
+#define SWARM_S256W_WAVES 6  // 80 VGPRs: three 512-thread workgroups per CU
+#endif
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SWARM_S256W_WAVES)))
+swarm_step256w(const S64Args args) {
+  (void)args;  // read through s64_args()
+  constexpr int KS = H_K + 1, MSL = H_MS + 1;
+  __shared__ H256WLds L;
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const bool primary = wv < 4;
+  const int w = wv & 3, t = threadIdx.x & 63;
+  const int i = 64 * w + t;  // drone
+  S64ArgPtr A = s64_args();
+  const int env = blockIdx.x;
+  if (env >= A->P.E) return;  // whole block
+  const int M = A->P.M;
+  const size_t ag = (size_t)env * H_N + i;
+  STAMP256(0);
+  STAMP_BEGIN(env, threadIdx.x == 0);
+
+  // ---- loads (the secondary: obstacles)
+  const int stepc = A->S.step_count[env];
+  const uint32_t episode0 = A->S.episode[env];
+  float gx = 0.f, gy = 0.f, gz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
+  float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f;
+  bool act = false, has = true;
+  if (primary) {
+    gx = A->S.goal[3 * env]; gy = A->S.goal[3 * env + 1]; gz = A->S.goal[3 * env + 2];
+    ax = A->actions[ag * 3]; ay = A->actions[ag * 3 + 1]; az = A->actions[ag * 3 + 2];
+    px = A->S.pos[ag * 3]; py = A->S.pos[ag * 3 + 1]; pz = A->S.pos[ag * 3 + 2];
+    vx = A->S.vel[ag * 3]; vy = A->S.vel[ag * 3 + 1]; vz = A->S.vel[ag * 3 + 2];
+    act = A->S.active[ag] != 0;
+    has = A->amask == nullptr || A->amask[ag] != 0;
+  } else if (i < M) {
+    const float* o = A->S.obstacles + ((size_t)env * M + i) * 3;
+    const float ox = o[0], oy = o[1], oz = o[2];
+    L.obst[i] = make_float4(ox, oy, oz, 0.f);
+    L.osoa[i] = ox; L.osoa[H_MMAX + i] = oy; L.osoa[2 * H_MMAX + i] = oz;
+  }
+  const int n_active = __syncthreads_count(act);
+  STAMP256(1);
+  A = s64_args();
+
+  // ---- integrate: drone_swarm_env.py:98-117 (swarm_kernel, DYN_KIN)
+  float prev_d = 0.f;
+  if (primary) {
+    if (act) {
+      prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
+      if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
+      ax = clampf(ax, -1.f, 1.f) * A->P.amax;
+      ay = clampf(ay, -1.f, 1.f) * A->P.amax;
+      az = clampf(az, -1.f, 1.f) * A->P.amax;
+      vx = vx + ax * A->P.dt;
+      vy = vy + ay * A->P.dt;
+      vz = vz + az * A->P.dt;
+      const float s_sp = sqsum_1d(vx, vy, vz);
+      if (!(s_sp <= A->P.s_vmax)) {
+        const float sp = sqrt_rn(s_sp);
+        if (!(sp <= A->P.vmax || sp < (float)1e-8)) {
+          vx = (vx / sp) * A->P.vmax;
+          vy = (vy / sp) * A->P.vmax;
+          vz = (vz / sp) * A->P.vmax;
+        }
+      }
+      px = px + vx * A->P.dt;
+      py = py + vy * A->P.dt;
+      pz = pz + vz * A->P.dt;
+    }
+    if (n_active > 0) {
+      px = clampf(px, A->P.neg_half_w, A->P.half_w);
+      py = clampf(py, A->P.neg_half_w, A->P.half_w);
+      pz = clampf(pz, A->P.neg_half_w, A->P.half_w);
+    }
+    hw_put(L, w, t, px, py, pz, act ? 1.f : 0.f);
+  }
+  const bool fast = __syncthreads_and(act || !primary) != 0;  // also the barrier after the puts
+  STAMP256(2);
+  A = s64_args();
+
+  // ---- formation + minimum pass (every pair once, split over the two waves), obstacle pass
+  double fsum = 0.0;
+  float smin = __builtin_inff();
+  uint32_t ok[MSL];
+#pragma unroll
+  for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
+  bool ocoll = false;
+  if (primary) {
+    if (fast) hw_pass1<true, true>(L, w, t, true, px, py, pz, A->P.ds_f, fsum, smin);
+    else hw_pass1<false, true>(L, w, t, act, px, py, pz, A->P.ds_f, fsum, smin);
+    obstacle_pass_s64<MSL, true>(L.osoa, M, px, py, pz, act, A->P.s_obst, A->P.ob_keep, ok, ocoll);
+  } else {
+    const float qx = L.seg2[w][0][t], qy = L.seg2[w][1][t], qz = L.seg2[w][2][t];
+    const bool self = L.seg2[w][3][t] != 0.f;
+    if (fast) hw_pass1<true, false>(L, w, t, true, qx, qy, qz, A->P.ds_f, fsum, smin);
+    else hw_pass1<false, false>(L, w, t, self, qx, qy, qz, A->P.ds_f, fsum, smin);
+  }
+  STAMP256(3);
+  __syncthreads();  // handed-over sums / minima written
+  if (primary) {
+    fsum += L.x.p1.dsum[i];
+    fsum += (double)L.x.p1.sum[0][i];
+    fsum += (double)L.x.p1.sum[1][i];
+    smin = fminf(fminf(smin, L.x.p1.mn[2][i]), fminf(L.x.p1.mn[0][i], L.x.p1.mn[1][i]));
+  }
+  A = s64_args();
+
+  STAMP256(4);
+  // ---- rewards / terminations: drone_swarm_env.py:120-172 (swarm_kernel, DYN_KIN)
+  float curr = 0.f, rew = 0.f;
+  bool reached = false, collided = false, term = false, trunc = false, cont = false;
+  bool term_all = false, trunc_all = false;
+  int new_step = stepc;
+  if (primary) {
+    bool pcoll = smin <= A->P.thr_pair * FAST_LO;
+    if (!pcoll && smin <= A->P.thr_pair * FAST_HI && act)
+      pcoll = exact_pair_collision(L.ring, H_N, i, px, py, pz, A->P.s_pair);
+    curr = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
+    bool p_coll = false, p_cand = false;
+    if (act) {
+      reached = (double)curr <= A->P.goal_radius;
+      collided = ocoll || pcoll;
+      p_coll = collided;
+      p_cand = !reached && !collided;
+      double r = ((double)prev_d - (double)curr) * A->P.kp;
+      if (n_active > 1) r = r + (-A->P.kf) * (fsum * inv_count(n_active - 1));
+      if (reached) r = r + A->P.r_goal;
+      if (collided) r = r + A->P.r_col;
+      rew = (float)r;
+    }
+    const bool wc = __ballot(p_coll) != 0, wd = __ballot(p_cand) != 0;
+    if (t == 0) L.red[w] = (wc ? 1u : 0u) | (wd ? 2u : 0u);
+  }
+  __syncthreads();
+  const uint32_t votes = L.red[0] | L.red[1] | L.red[2] | L.red[3];
+  const bool any_c = (votes & 1u) != 0, any_cand = (votes & 2u) != 0;
+  A = s64_args();
+  if (n_active == 0) {
+    term_all = true;
+  } else {
+    new_step = stepc + 1;
+    const bool tl = new_step >= A->P.max_steps;
+    term_all = (!any_cand && !any_c && !tl) || any_c;
+    trunc_all = tl && !term_all;
+    if (act) {
+      const bool done_i = reached || collided;
+      term = done_i;
+      trunc = tl && !done_i;
+      cont = !done_i && !tl && !any_c;
+    }
+  }
+  const bool do_reset = A->P.auto_reset && (term_all || trunc_all);
+  if (primary) {
+    A->O.reward[ag] = rew;
+    A->O.terminated[ag] = term ? 1 : 0;
+    A->O.truncated[ag] = trunc ? 1 : 0;
+    if (A->O.dist_goal) A->O.dist_goal[ag] = curr;
+    if (A->O.info_flags)
+      A->O.info_flags[ag] = (uint8_t)((act ? SWARM_AGENT_STEPPED : 0u) | (act && reached ? SWARM_AGENT_REACHED : 0u) |
+                                      (act && collided ? SWARM_AGENT_COLLISION : 0u) | (cont ? SWARM_AGENT_HAS_OBS : 0u));
+    if (i == 0)
+      A->O.env_done[env] = (uint8_t)((term_all ? SWARM_ENV_TERMINATED : 0u) | (trunc_all ? SWARM_ENV_TRUNCATED : 0u) |
+                                     (do_reset ? SWARM_ENV_RESET : 0u));
+  }
+
+  STAMP256(5);
+  // ---- in-kernel auto-reset (block-uniform): the new episode, then its keys
+  uint32_t episode_new = episode0;
+  if (do_reset) {
+    episode_new = episode0 + 1u;
+    const long long genv = A->P.env_offset + env;
+    const float lo_w = A->P.neg_half_w, wd_w = A->P.width_w;
+    float ox = 0.f, oy = 0.f, oz = 0.f;
+    if (primary) {
+      uint32_t wd4[4];
+      draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)i, wd4);
+      px = uni(wd4[0], lo_w, wd_w);
+      py = uni(wd4[1], lo_w, wd_w);
+      pz = uni(wd4[2], lo_w, wd_w);
+      vx = vy = vz = 0.f;
+      act = true;
+    } else if (i <= M) {  // obstacle i (i < M) or the goal (i == M)
+      uint32_t wo[4];
+      draw_block_k(A->P.seed_lo, A->P.seed_hi, genv, episode_new, (uint32_t)(H_N + i), wo);
+      ox = uni(wo[0], lo_w, wd_w); oy = uni(wo[1], lo_w, wd_w); oz = uni(wo[2], lo_w, wd_w);
+      if (i < M) {  // the state row: the old one was read into LDS at the start
+        float* o = A->S.obstacles + ((size_t)env * M + i) * 3;
+        o[0] = ox; o[1] = oy; o[2] = oz;
+      }
+    }
+    __syncthreads();  // every read of the old planes / ring / obstacles is done
+    if (primary) {
+      hw_put(L, w, t, px, py, pz, 1.f);
+    } else if (i < M) {
+      L.obst[i] = make_float4(ox, oy, oz, 0.f);
+      L.osoa[i] = ox; L.osoa[H_MMAX + i] = oy; L.osoa[2 * H_MMAX + i] = oz;
+    } else if (i == M) {
+      L.goal = make_float4(ox, oy, oz, 0.f);
+    }
+    __syncthreads();
+    if (primary) {
+      const float4 g4 = L.goal;
+      gx = g4.x; gy = g4.y; gz = g4.z;
+#pragma unroll
+      for (int s = 0; s < MSL; ++s) ok[s] = KEY_EMPTY;
+      bool c2 = false;
+      obstacle_pass_s64<MSL, false>(L.osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
+    }
+  }
+  STAMP256(6);
+  A = s64_args();
+  uint32_t nk[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
+  if (primary) {
+    hw_pass0<true>(L, w, t, px, py, pz, A->P.nb_keep, nk);
+  } else {
+    const float qx = L.seg2[w][0][t], qy = L.seg2[w][1][t], qz = L.seg2[w][2][t];
+    hw_pass0<false>(L, w, t, qx, qy, qz, A->P.nb_keep, nk);
+  }
+  __syncthreads();  // handed-over key lists written
+  if (!primary) return;  // no barrier follows
+  {
+    uint32_t kb[4], kc[4], ks2[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kb[s] = L.x.keys[0][s][i];
+      kc[s] = L.x.keys[1][s][i];
+      ks2[s] = L.x.keys[2][s][i];
+    }
+    h_merge4(nk, ks2);
+    h_merge4(nk, kb);
+    h_merge4(nk, kc);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) nk[s] = h_decode(nk[s], w, t, A->P.nb_keep);
+  }
+  A = s64_args();
+
+  // ---- exact top-K of the emitted observation (keys rank by s', drone indices)
+  float wd[KS], od[MSL];
+  int wj[KS], oj[MSL];
+  {
+    const uint32_t ff = h_finish_fast(nk, ok, L.ring, L.obst, M, A->P.nb_keep, A->P.ob_keep, px, py, pz, wd, wj, od, oj);
+    if (__ballot(ff != 0) != 0) {  // straight-line rest of finish_keys (s64_finish_general), then the scans
+      bool slow_nb, slow_ob;
+      s64_finish_general<KS, MSL, H_N, false, H_MMAX>(ff, nk, ok, L.ring, L.obst, i, M, A->P.nb_keep, A->P.ob_keep,
+                                                      false, px, py, pz, wd, wj, od, oj, slow_nb, slow_ob);
+      if (slow_nb) exact_select<KS, false>(L.ring, H_N, i, H_K, max_first(wd, H_K), px, py, pz, wd, wj);
+      if (slow_ob) exact_select<MSL, true>(L.obst, M, -1, H_MS, max_first(od, H_MS), px, py, pz, od, oj);
+    }
+  }
+  STAMP256(7);
+  A = s64_args();
+
+  // ---- state write-back
+  const bool new_act = do_reset || cont;
+  A->S.pos[ag * 3] = px; A->S.pos[ag * 3 + 1] = py; A->S.pos[ag * 3 + 2] = pz;
+  A->S.vel[ag * 3] = vx; A->S.vel[ag * 3 + 1] = vy; A->S.vel[ag * 3 + 2] = vz;
+  A->S.active[ag] = new_act ? 1 : 0;
+  if (i == 0) {
+    A->S.step_count[env] = do_reset ? 0 : new_step;
+    if (do_reset) {
+      A->S.episode[env] = episode_new;
+      A->S.goal[3 * env] = gx; A->S.goal[3 * env + 1] = gy; A->S.goal[3 * env + 2] = gz;
+    }
+  }
+  if (A->O.global_state) {
+    float* gs = A->O.global_state + (size_t)env * (6 * H_N + 3);
+    gs[3 * i] = px; gs[3 * i + 1] = py; gs[3 * i + 2] = pz;
+    gs[3 * H_N + 3 * i] = vx; gs[3 * H_N + 3 * i + 1] = vy; gs[3 * H_N + 3 * i + 2] = vz;
+    if (i == 0) { gs[6 * H_N] = gx; gs[6 * H_N + 1] = gy; gs[6 * H_N + 2] = gz; }
+  }
+  A = s64_args();
+
+  // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)], straight from registers
+  float* row = A->O.obs + ag * (9 + 4 * H_K + 4 * H_MS);
+  row[0] = px; row[1] = py; row[2] = pz;
+  row[3] = vx; row[4] = vy; row[5] = vz;
+  row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
+#pragma unroll
+  for (int s = 0; s < H_K; ++s) {
+    const float4 q = lds_f4(L.ring + (wj[s] & (H_N - 1)));
+    row[9 + 4 * s] = q.x - px; row[10 + 4 * s] = q.y - py; row[11 + 4 * s] = q.z - pz; row[12 + 4 * s] = wd[s];
+  }
+#pragma unroll
+  for (int s = 0; s < H_MS; ++s) {
+    const float4 q = lds_f4(L.obst + (oj[s] & (H_MMAX - 1)));
+    row[21 + 4 * s] = q.x - px; row[22 + 4 * s] = q.y - py; row[23 + 4 * s] = q.z - pz; row[24 + 4 * s] = od[s];
+  }
+  STAMP256(8);
+  STAMP_END(env, threadIdx.x == 0);
+}
 }  // namespace
 namespace swarm_dev {
 
@@ -3846,9 +4295,22 @@ __attribute__((visibility("hidden"))) void* swarm_pick_step64_eval();
 // the config-2 specialisation (SWARM_PART 6)
 __attribute__((visibility("hidden"))) void* swarm_pick_step16q();
 // the config-5 specialisation (SWARM_PART 7)
-__attribute__((visibility("hidden"))) void* swarm_pick_step256();
+// (kernel, threads per workgroup, LDS bytes): swarm_step256w (512 threads) unless SWARM_S256_WIDE=0
+__attribute__((visibility("hidden"))) void* swarm_pick_step256(int* threads, int* lds_bytes);
 #if SWARM_HAS_PART(7)
-__attribute__((visibility("hidden"))) void* swarm_pick_step256() { return reinterpret_cast<void*>(swarm_step256); }
+#ifndef SWARM_S256_WIDE
+#define SWARM_S256_WIDE 1
+#endif
+__attribute__((visibility("hidden"))) void* swarm_pick_step256(int* threads, int* lds_bytes) {
+  if (SWARM_S256_WIDE) {
+    *threads = 2 * swarm_dev::H_N;
+    *lds_bytes = (int)sizeof(swarm_dev::H256WLds);
+    return reinterpret_cast<void*>(swarm_step256w);
+  }
+  *threads = swarm_dev::H_N;
+  *lds_bytes = (int)sizeof(swarm_dev::H256Lds);
+  return reinterpret_cast<void*>(swarm_step256);
+}
 #endif
 #if SWARM_HAS_PART(6)
 __attribute__((visibility("hidden"))) void* swarm_pick_step16q() {
@@ -4219,8 +4681,9 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   }
   if (mode == MODE_STEP && step256_applies(p, kp) && !s->env_cfg) {
     const S64Args args{kp, *s, actions, amask, *o};
-    hipLaunchKernelGGL(reinterpret_cast<step64_fn>(swarm_pick_step256()), dim3(kp.E), dim3(H_N), 0,
-                       (hipStream_t)stream, args);
+    int threads = 0, lds = 0;
+    const step64_fn k256 = reinterpret_cast<step64_fn>(swarm_pick_step256(&threads, &lds));
+    hipLaunchKernelGGL(k256, dim3(kp.E), dim3(threads), 0, (hipStream_t)stream, args);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SWARM_OK;
@@ -4365,12 +4828,14 @@ int swarm_query_launch(const swarm_params_t* p, swarm_launch_info_t* info) {
     info->staged_obs = 0;
     info->kernel_id = SWARM_KERNEL_STEP16Q;
   }
-  if (rc == SWARM_OK && step256_applies(p, kp)) {  // one env per 256-thread workgroup, one lane per drone
+  if (rc == SWARM_OK && step256_applies(p, kp)) {  // one env per workgroup of 512 (or 256) threads
+    int threads = 0, lds = 0;
+    (void)swarm_pick_step256(&threads, &lds);
     info->lanes_per_env = H_N;
-    info->threads_per_block = H_N;
+    info->threads_per_block = threads;
     info->envs_per_block = 1;
     info->blocks = kp.E;
-    info->lds_bytes = (int)sizeof(H256Lds);
+    info->lds_bytes = lds;
     info->staged_obs = 0;
     info->kernel_id = SWARM_KERNEL_STEP256;
   }

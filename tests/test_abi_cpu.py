@@ -90,9 +90,10 @@ def test_launch_geometry(nat, lib, n):
         assert info.threads_per_block == 192 and info.envs_per_block == 1
         assert info.blocks == 1000 and 0 < info.lds_bytes <= 160 * 1024
         return
-    if info.kernel_id == nat.KERNEL_STEP256:  # config-5 specialisation: one env per 256-thread workgroup
+    if info.kernel_id == nat.KERNEL_STEP256:  # config-5 specialisation: one env per 512-thread workgroup
+        # (two waves per 64-drone block: swarm_step256w), one lane per drone in each half
         assert n == 256 and info.lanes_per_env == 256 and info.staged_obs == 0
-        assert info.threads_per_block == 256 and info.envs_per_block == 1
+        assert info.threads_per_block == 512 and info.envs_per_block == 1
         assert info.blocks == 1000 and 0 < info.lds_bytes <= 64 * 1024
         return
     assert info.lanes_per_env == lanes
