@@ -606,8 +606,8 @@ class VecSwarm:
             return "swarm_step64<32>"
         if kid == nat.KERNEL_STEP16Q:
             return "swarm_step16q"
-        if kid == nat.KERNEL_STEP256:
-            return "swarm_step256"
+        if kid == nat.KERNEL_STEP256:  # 512 threads: the two-waves-per-block build (swarm_step256w)
+            return "swarm_step256w" if int(li.threads_per_block) == 512 else "swarm_step256"
         if kid in (nat.KERNEL_STEP64, nat.KERNEL_STEP64_PERSISTENT):
             return "swarm_step64_phys_once<32, 4>" if self.dynamics == "physics" else "swarm_step64_once<32, 4>"
         lanes = int(li.lanes_per_env)

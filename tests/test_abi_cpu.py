@@ -113,7 +113,7 @@ def test_launch_geometry(nat, lib, n):
 
 def test_obs_direct_threshold(nat, lib):
     info = nat.SwarmLaunchInfo()
-    # (N = 16 / 256 with the default K / Ms / M run swarm_step16q / swarm_step256, rows from
+    # (N = 16 / 256 with the default K / Ms / M run swarm_step16q / swarm_step256w, rows from
     # registers at any E: the generic kernel's threshold is checked there with K = 4)
     for n, e, staged, extra in [(16, 1024, 0, {}), (16, 32768, 0, {}), (16, 1024, 0, {"neighbor_k": 4}),
                                 (16, 8192, 0, {"neighbor_k": 4}), (16, 8193, 1, {"neighbor_k": 4}),

@@ -46,7 +46,7 @@ def _snap(vec):
 def test_uniform_records_equal_no_records(dev, n, e, dyn, groups):
     from swarm_marl_amd import VecSwarm
     cfg = {"num_drones": n, "max_steps": 7}
-    # N = 16 / 256 without records run swarm_step16q / swarm_step256, whose rewards equal the
+    # N = 16 / 256 without records run swarm_step16q / swarm_step256w, whose rewards equal the
     # generic kernel's within 1e-5 only (formation partial sums in another order;
     # tests/test_gpu_step16.py, test_gpu_step256.py): compare the records path with the generic
     # kernel there

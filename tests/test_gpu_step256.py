@@ -1,5 +1,5 @@
-"""GPU: the config-5 specialisation swarm_step256 (N = 256, K = 3, Ms = 4, 4 <= M <= 16, kinematic;
-one env per 256-thread workgroup, every pair evaluated once) against the generic block-team kernel
+"""GPU: the config-5 specialisation swarm_step256w (N = 256, K = 3, Ms = 4, 4 <= M <= 16, kinematic;
+one env per 512-thread workgroup, every pair evaluated once, two waves per 64-drone block) against the generic block-team kernel
 swarm_kernel<0, 0, 4, 5, 0> (kernel_path="generic") on identical inputs — observations, flags,
 infos, global state and every state tensor bit-identical, rewards within the 1e-5 contract (the
 formation partial sums are added in a different order) — step after step with in-kernel
@@ -55,7 +55,7 @@ def test_kernel_selection(dev):
     from swarm_marl_amd import VecSwarm
     from swarm_marl_amd import _native as nat
     v = VecSwarm(4, {"num_drones": N}, device=dev)
-    assert int(v.launch_info.kernel_id) == nat.KERNEL_STEP256 and v.kernel_name() == "swarm_step256"
+    assert int(v.launch_info.kernel_id) == nat.KERNEL_STEP256 and v.kernel_name() == "swarm_step256w"
     for raw in ({"num_drones": 255}, {"num_drones": N, "neighbor_k": 4}, {"num_drones": N, "sensed_obstacles": 3},
                 {"num_drones": N, "num_obstacles": 3}, {"num_drones": N, "num_obstacles": 17}):
         assert int(VecSwarm(2, raw, device=dev).launch_info.kernel_id) == nat.KERNEL_GENERIC, raw
@@ -73,7 +73,7 @@ def test_step256_matches_generic_autoreset(dev, m, max_steps, masked, radii):
         raw.update(collision_radius=radii, goal_radius=radii, obstacle_radius=radii)
     e = 96
     a, b = _pair(dev, raw, e, auto_reset=True, seed=5, env_offset=3)
-    assert a.kernel_name() == "swarm_step256"
+    assert a.kernel_name() == "swarm_step256w"
     a.reset()
     b.reset()
     _assert_same(a, b, "reset")
@@ -146,7 +146,7 @@ def test_step256_vs_oracle(dev):
     cfg = oracle_cfg(raw)
     e = 6
     vec = VecSwarm(e, raw, device=dev, auto_reset=True, seed=21, with_infos=True, with_global_state=True)
-    assert vec.kernel_name() == "swarm_step256"
+    assert vec.kernel_name() == "swarm_step256w"
     vec.reset()
     torch.cuda.synchronize()
     st = vec_state_numpy(vec)
