@@ -3251,6 +3251,8 @@ struct H256Lds {
 // half-wave's two copies land on disjoint banks), so each lane reads aligned rotation pairs.
 constexpr int H_C1 = 158;
 constexpr int H_PS = 288;  // dwords per plane: copy 0 [0, 128), copy 1 [H_C1 + 1, H_C1 + 129)
+static_assert(H_C1 % 64 == 30 && H_C1 % 2 == 0 && H_PS % 2 == 0 && H_C1 >= 2 * 64 && H_C1 + 1 + 2 * 64 <= H_PS,
+              "two-copy plane layout: copy 1 even-based, 30 banks after copy 0, both copies inside the plane");
 struct H256WLds {
   float seg2[4][4][H_PS];
   float4 ring[H_N];
