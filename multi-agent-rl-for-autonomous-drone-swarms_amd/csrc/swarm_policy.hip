@@ -536,6 +536,28 @@ policy_mlp_x3(const FwdArgs A) {
   const long long ntiles = (A.rows + 31) / 32;
   const float* b2 = reinterpret_cast<const float*>(lds + L.b2);
   const float* b3 = reinterpret_cast<const float*>(lds + L.b3);
+  // The next tile's observations, requested in the tail of the current tile (after its last
+  // layer-2 MFMAs, when h1 is dead) so that the next tile starts on landed data: one wave per SIMD
+  // has nothing else to hide that load's latency with (~26 us of 262 without it, r05ai).  The index
+  // is clamped rather than branched on, so the values are redefined on every path and dead
+  // between their use and the refill.
+  float xvn[KS1 * 8];
+  auto request_obs = [&](long long tl, int n_, int h_, int in_) {
+    const long long r = tl * 32 + n_;
+    const float* xr = A.obs + (r < A.rows ? r : A.rows - 1) * in_;
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 16 * ks + 8 * h_ + j;
+        xvn[ks * 8 + j] = xr[k < in_ ? k : in_ - 1];
+      }
+  };
+  {
+    const long long t0 = (long long)blockIdx.x * WAVES + wave;
+    const int ln = threadIdx.x & 63;
+    request_obs(t0 < ntiles ? t0 : 0, ln & 31, (ln >> 5) & 1, IN_C ? IN_C : A.in);
+  }
   for (long long tile = (long long)blockIdx.x * WAVES + wave; tile < ntiles; tile += (long long)gridDim.x * WAVES) {
     int lane = threadIdx.x & 63, in_r = A.in, out_r = A.out;
     uint32_t sb = 0;
@@ -553,15 +575,10 @@ policy_mlp_x3(const FwdArgs A) {
     // ---- obs fragments, split: x[row][16 ks + 8 h + j], x[in] = 1 (bias column)
     f16x8 xh[KS1], xl[KS1];
     {
-      const float* xr = A.obs + (valid ? row : A.rows - 1) * in;
+      (void)valid;
       float xv[KS1 * 8];
 #pragma unroll
-      for (int ks = 0; ks < KS1; ++ks)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = 16 * ks + 8 * h + j;
-          xv[ks * 8 + j] = xr[k < in ? k : in - 1];
-        }
+      for (int i = 0; i < KS1 * 8; ++i) xv[i] = xvn[i];
 #pragma unroll
       for (int ks = 0; ks < KS1; ++ks)
 #pragma unroll
@@ -583,7 +600,13 @@ policy_mlp_x3(const FwdArgs A) {
     f32x16 l1acc[2], l1accx[2];
     auto epi1 = [&](int pob, int part) {
       if (part == 0) l1acc[pob & 1] = x3_sum(l1acc[pob & 1], l1accx[pob & 1]);
-      else split8(l1acc[pob & 1], part - 1, true, h1h[2 * pob + part - 1], h1l[2 * pob + part - 1]);
+      else {
+        split8(l1acc[pob & 1], part - 1, true, h1h[2 * pob + part - 1], h1l[2 * pob + part - 1]);
+        // h1 lo lives in AGPRs (MFMA B operands may come from AGPRs): 64 architectural VGPRs
+        // freed for the observation request above (without it the kernel sits at the 256-VGPR cap
+        // and that request spills, r05aj)
+        asm volatile("" : "+a"(h1l[2 * pob + part - 1]));
+      }
     };
 #pragma unroll
     for (int ob = 0; ob < OB; ++ob) {
@@ -675,6 +698,10 @@ policy_mlp_x3(const FwdArgs A) {
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    {  // h1 is dead: the next tile's observations
+      const long long nt = tile + (long long)gridDim.x * WAVES;
+      request_obs(nt < ntiles ? nt : tile, n, h, in);
+    }
     // the last block's epilogue
     epi(OB - 1, 0);
     epi(OB - 1, 1);
@@ -712,8 +739,9 @@ constexpr int BF16_TILES = 1;
 constexpr int BF16_WAVES_T = 8;
 constexpr int F32_WAVES = 4;
 // f32x3: waves per workgroup (one workgroup per CU: the LDS blob); 4 = one wave per SIMD: the hi
-// and lo fragments of h1 (128 VGPRs), three accumulator chains and the double-buffered W2 lo
-// batches need ~330 registers (at 2 waves per SIMD, 256, it spills)
+// and lo fragments of h1 (128 registers, lo in AGPRs), the accumulator chains, the double-buffered
+// W2 lo batches and the next tile's observations need ~380 registers (at 2 waves per SIMD, 256,
+// it spills)
 constexpr int X3_WAVES = 4;
 
 thread_local char g_perr[256] = "";
