@@ -167,3 +167,21 @@ def test_step256_vs_oracle(dev):
         for k in ("pos", "vel", "goal", "obst", "active", "step", "episode"):
             assert np.array_equal(got[k], st[k]), f"state {k} t={t}"
         assert np.array_equal(vec.global_state.cpu().numpy(), out["global_state"])
+
+
+@pytest.mark.parametrize("e,groups", [(1, 1), (1030, 3)])
+def test_step256_single_env_and_groups(dev, e, groups):
+    """One env (one 512-thread workgroup), and a batch split into env groups of unequal size on
+    their own streams (swarm_step_groups) — against the generic kernel step after step."""
+    raw = dict(num_drones=N, max_steps=7)
+    a, b = _pair(dev, raw, e, auto_reset=True, seed=13, groups=groups)
+    assert a.kernel_name() == "swarm_step256w"
+    a.reset()
+    b.reset()
+    g = torch.Generator(device=dev).manual_seed(19)
+    for t in range(3):
+        act = torch.rand((e, N, 3), device=dev, generator=g) * 2 - 1
+        a.step(act)
+        b.step(act)
+        torch.cuda.synchronize()
+        _assert_same(a, b, f"E={e} groups={groups} t={t}")
