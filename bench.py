@@ -100,8 +100,6 @@ def parse(argv=None):
                     help="one workgroup per env instead of the persistent env queue")
     ap.add_argument("--no-graph", action="store_true",
                     help="time the whole-job rate with eager launches instead of hipGraph replay")
-    ap.add_argument("--use-graph", action="store_true",
-                    help="hipGraph replay for K > 256 even where the preset times eager launches (n16)")
     ap.add_argument("--ctde", action="store_true", default=None,
                     help="also emit global_state and all-gather it (config 5)")
     ap.add_argument("--no-ctde", dest="ctde", action="store_false",
@@ -158,8 +156,6 @@ def parse(argv=None):
     a.envs = pre["envs"] if a.envs is None else a.envs
     a.ctde = pre["ctde"] if a.ctde is None else a.ctde
     a.label = pre["label"]
-    if not pre.get("graph", True) and not a.use_graph:
-        a.no_graph = True
     a.groups_explicit = a.groups is not None
     if a.groups is None:
         # 4 groups where the timed region replays graphs (K > 256, no CTDE gather): 25.2 vs
@@ -320,6 +316,41 @@ def profile_record(workload_key: str):
         return None
 
 
+def valu_roofline(prof: dict, kern_ms: float) -> dict:
+    """VALU side of the roofline from the committed PMC record of this workload (not measured in
+    this run) against this run's step time `kern_ms` (one step = every env of the GPU once):
+    * frac_2cycle: SQ_INSTS_VALU x 64 lanes against VALU_PEAK_LANE_OPS (every instruction at the
+      full, 2-cycle rate): a LOWER bound, since about half of the step's instructions are
+      half-rate encodings (min / max / med3, packed f32, DPP, compares, f64, conversions);
+    * busy_class_costed [lo, hi]: per-SIMD VALU issue time (the PMC instruction classes priced at
+      their cheapest / dearest member's measured ns per wave-instruction per SIMD, tools/valu_busy.py,
+      profiles/r05o_valu_rate4.txt) / step time; busy_frac = hi (the occupancy sweep's measured
+      marginal cost per wave, DESIGN.md §6, lands at the top of the bracket);
+    * counter_frac: 4 x SQ_ACTIVE_INST_VALU (quad-cycles per wave, summed over the step's waves)
+      / (SIMDs x step time x 2.4 GHz) — the counter charges one quad-cycle per VALU instruction,
+      so it reads as a 4-cycle model at the nominal clock."""
+    lane_ops = prof["valu_insts_per_launch"] * 64.0
+    out = {"frac_2cycle": lane_ops / (kern_ms * 1e-3) / VALU_PEAK_LANE_OPS,
+           "achieved_lane_ops_per_s": lane_ops / (kern_ms * 1e-3), "peak_lane_ops_per_s": VALU_PEAK_LANE_OPS,
+           "frac_2cycle_note": "lower bound: SQ_INSTS_VALU x 64 lanes at 32 lanes/clk/SIMD (a wave64 "
+                               "instruction at the full 2-cycle rate) x 1024 SIMDs x 2.4 GHz",
+           "valu_insts_per_wave": prof.get("valu_insts_per_wave")}
+    waves, simds = prof.get("waves"), prof.get("simds", 1024)
+    ns = prof.get("valu_issue_ns_per_wave")
+    if waves and ns:
+        per_simd_us = [x * waves / simds * 1e-3 for x in ns]
+        out["valu_issue_us_per_simd_per_step"] = [round(x, 3) for x in per_simd_us]
+        out["busy_class_costed"] = [x / (kern_ms * 1e3) for x in per_simd_us]
+        out["busy_frac"] = out["busy_class_costed"][1]
+    act = prof.get("active_inst_valu_per_wave")
+    if waves and act:
+        out["counter_frac"] = 4.0 * act * waves / simds / (kern_ms * 1e-3 * 2.4e9)
+    out["source"] = (f"profiles/pmc_traffic.json (rounds {prof.get('round')} / {prof.get('valu_class_round')}); "
+                     "class prices from profiles/r05o_valu_rate4.txt; python tools/valu_busy.py "
+                     f"{prof.get('valu_class_round')} reproduces the per-wave figures")
+    return out
+
+
 # ----------------------------------------------------------------------------- main
 def main(argv=None):
     import torch
@@ -334,6 +365,9 @@ def main(argv=None):
     rehearsal = os.environ.get("SWARM_BENCH_REHEARSAL") == "1"
     if world > 1:
         if not rehearsal:
+            if torch.cuda.device_count() < world:  # the launcher parent did not open the GPU to check
+                raise SystemExit(f"bench.py rank {rank}: {world} ranks need {world} GPUs (one per rank), "
+                                 f"{torch.cuda.device_count()} visible")
             torch.cuda.set_device(local)
         dist.init_process_group("gloo" if rehearsal else "nccl")
     dev = torch.device("cuda", local if world > 1 and not rehearsal else 0)
@@ -732,13 +766,12 @@ def main(argv=None):
                 "grid": int(vec.group_launch_info[0].blocks),
                 "env_groups": G, "launches_per_step": G}
         if prof.get("valu_insts_per_launch"):
-            lane_ops = prof["valu_insts_per_launch"] * 64.0
-            roof["valu"] = {"achieved_lane_ops_per_s": lane_ops / (kern_max * 1e-3),
-                            "peak": VALU_PEAK_LANE_OPS,
-                            "frac": lane_ops / (kern_max * 1e-3) / VALU_PEAK_LANE_OPS,
-                            "source": "SQ_INSTS_VALU x 64 lanes from profiles/pmc_traffic.json; peak = "
-                                      "32 lanes/clk/SIMD (a wave64 instruction holds its SIMD-32 for 2 cycles) "
-                                      "x 1024 SIMDs x 2.4 GHz"}
+            roof["valu"] = valu_roofline(prof, kern_max)
+            busy = roof["valu"].get("busy_frac")
+            if busy is not None and busy > roof["frac"]:
+                roof["bound"] = "valu"
+                roof["bound_note"] = ("the SIMDs' VALU issue (roofline.valu.busy_frac, class-costed) is busier "
+                                      "than HBM (frac); achieved / peak / unit / frac stay the HBM figures")
         metric = METRIC if pol is None else \
             "rollout agent-steps/sec (on-device policy + env step) at N=64 x E=8192 per MI355X"
         if tracker is not None:
@@ -833,12 +866,28 @@ def check_world(gpus: int, env=None, device_count=None) -> tuple[int, str | None
         world, mode = gpus, ("launch" if gpus > 1 else None)
     if not shared:
         if device_count is None:
-            import torch  # counting devices does not initialise the GPU on this image
-            device_count = torch.cuda.device_count()
+            # the launcher parent never loads the HIP runtime (a child counts the devices; every
+            # rank checks again before it touches its GPU, main()); a single rank counts itself
+            device_count = count_devices_child() if mode == "launch" else _count_devices()
         if device_count < world:
             raise SystemExit(f"bench.py: --gpus {gpus} needs {world} GPUs (one rank per GPU), "
                              f"{device_count} visible")
     return world, mode
+
+
+def _count_devices() -> int:
+    import torch
+    return torch.cuda.device_count()
+
+
+def count_devices_child() -> int:
+    """Visible GPUs, counted in a short-lived child process so that the launcher parent never
+    imports torch or maps the HIP runtime before it starts the ranks."""
+    p = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    if p.returncode != 0:
+        raise SystemExit(f"bench.py: counting GPUs failed ({p.returncode}): {p.stderr[-500:]}")
+    return int(p.stdout.strip().splitlines()[-1])
 
 
 def launch_ranks(gpus: int, argv) -> int:
@@ -912,14 +961,37 @@ def standin_main(args) -> None:
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
+    if os.environ.get("SWARM_BENCH_STANDIN_FAIL_RANK") == str(rank):
+        # tests: this rank fails while the others wait for it in the timed region's barrier
+        raise SystemExit(f"stand-in rank {rank}: failing on request (SWARM_BENCH_STANDIN_FAIL_RANK)")
     offset, e = shard_plan(world, rank, args.envs)
     x = torch.zeros((e, args.drones, 3))
+    # --ctde with several ranks: main()'s CTDE branch — a global_state slot ring written by every
+    # step and all-gathered every --gather-every steps (distributed.GlobalStateGather over gloo)
+    gatherer, gathers, ring, seen = None, set(), None, []
+    if args.ctde and world > 1:
+        from swarm_marl_amd.distributed import GlobalStateGather
+        ring = torch.zeros((args.gs_slots, e, 6 * args.drones + 3))
+        gatherer = GlobalStateGather(ring, lambda i: None, keep=2)
+        gathers = set(gather_schedule(args.steps, args.gather_every))
+
+    def step(k):
+        x.add_(1.0)
+        if gatherer is None:
+            return
+        s = gatherer.before_step()
+        ring[s].fill_(float(1000 * rank + k))  # the step's global_state write-back
+        gatherer.after_step(gather=k in gathers)
+        if k in gathers:  # rank order of the concatenation (the values say which rank and step)
+            out = gatherer.result()
+            seen.append(bool(all(float(out[r * e, 0]) == 1000 * r + k for r in range(world))))
 
     def body():
-        for _ in range(args.steps):
-            x.add_(1.0)
-    for _ in range(args.warmup):
+        for k in range(args.steps):
+            step(k)
+    for k in range(args.warmup):
         x.add_(1.0)
+    gather_t0 = gatherer.k if gatherer is not None else 0
     wall = timed_region(body, world, lambda: None)
     (wall_max,) = max_over_ranks([wall], world)
     devs = rank_devices(world, {"rank": rank, "device": "cpu", "env_offset": offset})
@@ -932,7 +1004,13 @@ def standin_main(args) -> None:
                           "standin": "CPU stand-in step (SWARM_BENCH_STANDIN=cpu): rank plumbing only, "
                                      "not a measurement",
                           "config": {"workload": f"N={args.drones} drones x E={e} envs per rank (stand-in)",
-                                     "global_envs": world * e, "parallelism": f"env-sharded x{world}"}}),
+                                     "global_envs": world * e, "parallelism": f"env-sharded x{world}",
+                                     "ctde_allgather": gatherer is not None,
+                                     "ctde_gather_every": args.gather_every if gatherer is not None else None,
+                                     "ctde_gathers_timed": (sum(1 for k in gatherer.gathered_steps if k >= gather_t0)
+                                                            if gatherer is not None else None),
+                                     "ctde_gather_backend": gatherer.backend if gatherer is not None else None,
+                                     "ctde_rank_order_ok": all(seen) if gatherer is not None else None}}),
               flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -172,7 +172,108 @@ def test_check_world_rules():
 
 @pytest.mark.timeout(300)
 def test_launcher_fails_when_a_rank_fails():
-    """A rank that fails makes the launcher exit non-zero (rank 1 gets a bad env count)."""
-    p = _run_bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--envs", "-1"],
-                   {"SWARM_BENCH_STANDIN": "cpu"})
+    """Only rank 1 fails; rank 0 is then blocked in the timed region's barrier and must be stopped
+    by the launcher, which exits non-zero well inside the timeout (gloo's own barrier timeout is
+    30 minutes)."""
+    import time
+    t0 = time.perf_counter()
+    p = _run_bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--envs", "4"],
+                   {"SWARM_BENCH_STANDIN": "cpu", "SWARM_BENCH_STANDIN_FAIL_RANK": "1"}, timeout=200)
     assert p.returncode != 0
+    assert "rank 1 exited" in p.stderr, p.stderr[-2000:]
+    assert not [s for s in p.stdout.splitlines() if s.startswith("{")]  # rank 0 never reported
+    assert time.perf_counter() - t0 < 150
+
+
+_PARENT_PROBE = r"""
+import json, subprocess, sys
+sys.argv = ["bench.py", *sys.argv[1:]]
+import bench
+real = subprocess.Popen
+seen = []
+class Spy(real):
+    def __init__(self, cmd, *a, **k):
+        # the parent's state at every child it starts: the device-count child and each rank
+        maps = open("/proc/self/maps").read()
+        torch_in = "torch" in sys.modules
+        cuda_init = bool(torch_in and sys.modules["torch"].cuda.is_initialized())
+        seen.append({"cmd": " ".join(map(str, cmd))[-60:], "torch_imported": torch_in,
+                     "cuda_initialized": cuda_init, "hip_mapped": "libamdhip64" in maps})
+        super().__init__(cmd, *a, **k)
+subprocess.Popen = Spy
+msg = ""
+try:
+    rc = bench.entry()
+except SystemExit as e:
+    rc = 1 if e.code is None or isinstance(e.code, str) else e.code
+    msg = str(e.code)
+print("PROBE " + json.dumps({"rc": rc, "msg": msg, "seen": seen}), file=sys.stderr)
+sys.exit(0)
+"""
+
+
+def _probe(args, env_extra):
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    ROOT = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra, PYTHONPATH=str(ROOT))
+    p = subprocess.run([sys.executable, "-c", _PARENT_PROBE, *args], env=env, cwd=str(ROOT),
+                       capture_output=True, text=True, timeout=240)
+    line = [s for s in p.stderr.splitlines() if s.startswith("PROBE ")]
+    assert line, p.stderr[-2000:]
+    return json.loads(line[-1][6:]), p
+
+
+@pytest.mark.timeout(300)
+def test_launcher_parent_never_initialises_hip():
+    """The launcher branch of `python bench.py --gpus N`: at every child it starts (the device-count
+    child, then the ranks) the parent has not imported torch, so torch.cuda is not initialised and
+    libamdhip64 is not mapped (exec-after-HIP-init is forbidden on the GPU pool, and a parent holding
+    a HIP context would share the card with its ranks)."""
+    # no GPU here: the device-count child reports 0 and the launch stops before any rank starts
+    r, p = _probe(["--gpus", "2", "--steps", "2"], {})
+    assert r["rc"] != 0 and "needs 2 GPUs" in r["msg"]
+    assert len(r["seen"]) == 1 and "device_count" in r["seen"][0]["cmd"]
+    # the CPU stand-in skips the count: the parent starts both ranks, still HIP-free
+    r, p = _probe(["--gpus", "2", "--steps", "2", "--warmup", "1", "--envs", "4"], {"SWARM_BENCH_STANDIN": "cpu"})
+    assert r["rc"] == 0, p.stderr[-2000:]
+    assert len(r["seen"]) == 2
+    for s in r["seen"]:
+        assert not s["torch_imported"] and not s["cuda_initialized"] and not s["hip_mapped"], s
+
+
+@pytest.mark.timeout(300)
+def test_standin_ctde_gpus2_gathers():
+    """`bench.py --config n256 --ctde --gpus 2` on the CPU stand-in: main()'s CTDE branch — the
+    global_state slot ring all-gathered over gloo every --gather-every steps inside the timed
+    region, shards concatenated in rank order."""
+    import json
+    p = _run_bench(["--config", "n256", "--ctde", "--gpus", "2", "--steps", "10", "--warmup", "1",
+                    "--envs", "4", "--gather-every", "4"], {"SWARM_BENCH_STANDIN": "cpu"})
+    assert p.returncode == 0, p.stderr[-2000:]
+    rec = [json.loads(s) for s in p.stdout.splitlines() if s.startswith("{")]
+    assert len(rec) == 1
+    c = rec[0]["config"]
+    assert c["ctde_allgather"] is True and c["ctde_gather_backend"] == "gloo"
+    assert c["ctde_gathers_timed"] == len([3, 7, 9]) and c["ctde_rank_order_ok"] is True
+    assert rec[0]["world_size"] == 2 and c["global_envs"] == 8
+
+
+def test_valu_roofline_from_committed_pmc():
+    """bench.valu_roofline: the committed PMC record of the headline gives the 2-cycle lower bound,
+    the class-costed busy bracket and the SQ_ACTIVE_INST_VALU figure; the line's bound becomes
+    "valu" when the class-costed busy fraction exceeds the HBM fraction (round-5 review ask)."""
+    import json
+    from pathlib import Path
+    import bench
+    prof = json.loads((Path(bench.ROOT) / "profiles" / "pmc_traffic.json").read_text())["kinematic+swarm N=64 E=8192"]
+    v = bench.valu_roofline(prof, 0.0227)
+    lo, hi = v["busy_class_costed"]
+    assert v["frac_2cycle"] < lo <= hi == v["busy_frac"]
+    assert 0.3 < hi < 1.2 and 0.3 < v["counter_frac"] < 1.2
+    assert "lower bound" in v["frac_2cycle_note"]
+    # per-SIMD issue time: waves per SIMD x ns per wave
+    assert abs(v["valu_issue_us_per_simd_per_step"][1] - prof["valu_issue_ns_per_wave"][1] * 8e-3) < 1e-2
