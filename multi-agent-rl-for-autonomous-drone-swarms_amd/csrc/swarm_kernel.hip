@@ -33,6 +33,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <type_traits>
 
 #include "swarm_mi355x.h"
 
@@ -57,6 +58,15 @@
 // Tuning constants (each measured against its alternatives)
 constexpr int FB_BATCH = 8;            // exact scans: LDS reads in flight per batch
 constexpr int S64_PAIR_BATCH = 4;      // step64 pair pass: rotations per scheduling group
+#ifndef SWARM_S64_F32SUM
+#define SWARM_S64_F32SUM 1  // step64 formation sum: one f32 chain per pass, widened once
+#endif
+#ifndef SWARM_OBST_OMIN
+#define SWARM_OBST_OMIN 1  // obstacle passes: collisions from the running minimum (no exec-mask chain)
+#endif
+#ifndef SWARM_S64_BIGSQRT
+#define SWARM_S64_BIGSQRT 1  // step64 finish: square roots without the tiny-input branch when the keys prove it
+#endif
 constexpr int S64_CH_ROWS = 32;        // step64 obs rows per LDS staging chunk
 constexpr int S64_WG_ENVS_C = 4;       // step64: one-env waves per workgroup
 constexpr int S64_EVAL_WAVES = 8;      // step64 with the fused eval: waves per EU
@@ -155,6 +165,11 @@ __device__ __forceinline__ float sqrt_rn_nb(float x, bool& tiny) {
   r = (em <= 0.0f) ? rm : r;
   r = (ep > 0.0f) ? rp : r;
   return r;
+}
+// sqrt_rn for an input the caller proved is 0 or >= 2^-96 (no slow-path test, no branch)
+__device__ __forceinline__ float sqrt_rn_big(float x) {
+  bool unused = false;
+  return sqrt_rn_nb(x, unused);
 }
 __device__ __forceinline__ double dsqrt_rn(double x) { return __builtin_sqrt(x); }
 // np.linalg.norm(v) of a float32 3-vector: OpenBLAS sdot = double accumulation of float
@@ -1379,10 +1394,10 @@ typedef float s64_f2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(3))) float s64_lds_cf;
 typedef __attribute__((address_space(1))) uint8_t s64_gu8;
 // F0: key slots filled before this group (the list starts empty at the pass's first group)
-template <int KS, int PASS, bool FAST, int RT, int NB, bool MIRROR, int F0 = (KS > 0 ? KS : 1)>
+template <int KS, int PASS, bool FAST, int RT, int NB, bool MIRROR, int F0 = (KS > 0 ? KS : 1), class FS = double>
 __device__ __forceinline__ void pair_group_s64(s64_lds_cf* __restrict__ s0, uint32_t t4, float px, float py, float pz,
                                                bool self, uint32_t sflag, uint32_t keep, uint32_t keep_m, float ds,
-                                               uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum,
+                                               uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, FS& fsum,
                                                float& macc) {
   float sq[NB], term[NB];
   bool el[NB];
@@ -1467,20 +1482,20 @@ __device__ __forceinline__ void pair_group_s64(s64_lds_cf* __restrict__ s0, uint
       for (int i = 0; i < NB; ++i) macc = wave_ror1(macc) + term[i];
     }
   }
-  if constexpr (PASS == 1) fsum += (double)esum;
+  if constexpr (PASS == 1) fsum += (FS)esum;
 }
-template <int KS, int PASS, bool FAST, int RT, int B, int F0 = (KS > 0 ? KS : 1)>
+template <int KS, int PASS, bool FAST, int RT, int B, int F0 = (KS > 0 ? KS : 1), class FS = double>
 __device__ __forceinline__ void pair_groups_s64(s64_lds_cf* __restrict__ s0, uint32_t t4, float px, float py, float pz,
                                                 bool self, uint32_t sflag, uint32_t keep, uint32_t keep_m, float ds,
-                                                uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, double& fsum,
+                                                uint32_t (&nk)[KS > 0 ? KS : 1], float& smin, FS& fsum,
                                                 float& macc) {
   if constexpr (RT >= 1) {
     constexpr int NB = RT < B ? RT : B;
     constexpr int F1 = F0 + 2 * NB < KS ? F0 + 2 * NB : (KS > 0 ? KS : 1);
-    pair_group_s64<KS, PASS, FAST, RT, NB, true, F0>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum,
-                                                     macc);
-    pair_groups_s64<KS, PASS, FAST, RT - NB, B, F1>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin,
-                                                    fsum, macc);
+    pair_group_s64<KS, PASS, FAST, RT, NB, true, F0, FS>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin,
+                                                         fsum, macc);
+    pair_groups_s64<KS, PASS, FAST, RT - NB, B, F1, FS>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin,
+                                                        fsum, macc);
   }
 }
 // `soa` = the wave's pair-pass ring (S64Lds::soa); lane t reads from soa + t.
@@ -1497,13 +1512,20 @@ __device__ __forceinline__ void pair_pass_s64(const float* __restrict__ soa, int
   s64_lds_cf* s0 = (s64_lds_cf*)(soa + t);
   asm volatile("" : "+v"(s0));
   float macc = 0.f;
+  // the formation sum: one f32 chain over the pass (own terms group by group, the travelled mirror
+  // sum, rotation 32), widened once — the f64 add per 4-rotation group cost a conversion and an
+  // f64 add (both half rate) each; the sum's rounding stays ~1e-6 of the reward (1e-5 contract,
+  // the mirror sum was already one f32 chain)
+  using FS = typename std::conditional<SWARM_S64_F32SUM != 0, float, double>::type;
+  FS fs = 0;
   // every caller starts the pass with an empty key list (F0 = 0)
-  pair_groups_s64<KS, PASS, FAST, 31, S64_PAIR_BATCH, 0>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk,
-                                                           smin, fsum, macc);
-  if constexpr (PASS == 1) fsum += (double)wave_ror1(macc);
+  pair_groups_s64<KS, PASS, FAST, 31, S64_PAIR_BATCH, 0, FS>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk,
+                                                               smin, fs, macc);
+  if constexpr (PASS == 1) fs += (FS)wave_ror1(macc);
   // rotation 32 pairs t with t+32 from both sides: own evaluation only
-  pair_group_s64<KS, PASS, FAST, 32, 1, false>(s0, t4, px, py, pz, self, sflag, keep, keep_m, ds, nk, smin, fsum,
-                                               macc);
+  pair_group_s64<KS, PASS, FAST, 32, 1, false, (KS > 0 ? KS : 1), FS>(s0, t4, px, py, pz, self, sflag, keep, keep_m,
+                                                                      ds, nk, smin, fs, macc);
+  if constexpr (PASS == 1) fsum += (double)fs;
 }
 // step64's obstacle pass: obstacle_pass's exact axis-path squared sums ((x*x + y*y) + z*z, no
 // FMA) and keys for two obstacles per packed-f32 operation, from the obstacle planes `os`
@@ -1518,6 +1540,10 @@ __device__ __forceinline__ void obstacle_pass_s64(const float* __restrict__ os, 
   s64_f2 X = {os[0], os[1]};
   s64_f2 Y = {os[S64_MMAX], os[S64_MMAX + 1]};
   s64_f2 Z = {os[2 * S64_MMAX], os[2 * S64_MMAX + 1]};
+  // collisions: the running minimum of s over the obstacles (one v_min3_f32 per two) against
+  // the threshold once at the end — the same boolean as a per-obstacle compare, without the
+  // short-circuit exec-mask branches a `coll || ...` chain compiles to
+  float omin = __builtin_inff();
   // `filled`: key slots filled before pair m (the list starts empty; the first two pairs are
   // peeled, M >= 4 for every caller: Ms = 4 <= M)
   auto pair = [&](int filled) {
@@ -1534,7 +1560,10 @@ __device__ __forceinline__ void obstacle_pass_s64(const float* __restrict__ os, 
       kins_n<MSL>(ok, (__float_as_uint(sq.x) & keep) | (uint32_t)m, filled);
       kins_n<MSL>(ok, (__float_as_uint(sq.y) & keep) | (uint32_t)(m + 1), filled + 1);
     }
-    if constexpr (COLL) coll = coll || (chk && ((sq.x <= s_thr) || (sq.y <= s_thr)));
+    if constexpr (COLL) {
+      if constexpr (SWARM_OBST_OMIN) omin = fminf(omin, fminf(sq.x, sq.y));
+      else coll = coll || (chk && ((sq.x <= s_thr) || (sq.y <= s_thr)));
+    }
   };
   pair(0);
   m = 2;
@@ -1543,8 +1572,12 @@ __device__ __forceinline__ void obstacle_pass_s64(const float* __restrict__ os, 
   if (m < M) {
     const float sq = sqsum_f(os[m] - px, os[S64_MMAX + m] - py, os[2 * S64_MMAX + m] - pz);
     if constexpr (MSL > 0) kins<MSL>(ok, (__float_as_uint(sq) & keep) | (uint32_t)m);
-    if constexpr (COLL) coll = coll || (chk && (sq <= s_thr));
+    if constexpr (COLL) {
+      if constexpr (SWARM_OBST_OMIN) omin = fminf(omin, sq);
+      else coll = coll || (chk && (sq <= s_thr));
+    }
   }
+  if constexpr (COLL && SWARM_OBST_OMIN) coll = coll || (chk && omin <= s_thr);
 }
 __device__ __forceinline__ void s64_put_obst(float4* __restrict__ obst, float* __restrict__ os, int t, float ox,
                                              float oy, float oz) {
@@ -1579,7 +1612,9 @@ __device__ __forceinline__ void s64_put(float4* __restrict__ ring, float* __rest
 // Flags of s64_finish_fast (per lane): a near-tie among the neighbour / obstacle survivors, and
 // the survivor bound failing on either side.
 constexpr uint32_t S64F_NEAR_NB = 1u, S64F_NEAR_OB = 2u, S64F_BOUND_NB = 4u, S64F_BOUND_OB = 8u;
-template <int KS, int MSL>
+// BIG: the caller proved every survivor's squared distance is 0 or >= 2^-96 (sqrt_rn_big: the
+// exact square roots without sqrt_rn's per-call wave test and branch, one basic block)
+template <int KS, int MSL, bool BIG = false>
 __device__ __forceinline__ uint32_t s64_finish_fast(const uint32_t (&nk)[KS], const uint32_t (&ok)[MSL],
                                                     const float4* __restrict__ ring, const float4* __restrict__ obst,
                                                     int t, int M, uint32_t nb_keep, uint32_t ob_keep, bool dkey,
@@ -1600,7 +1635,7 @@ __device__ __forceinline__ uint32_t s64_finish_fast(const uint32_t (&nk)[KS], co
     const int j = (t + (int)(nk[s] & nim)) & (S64_N - 1);
     const float4 q = s64_ring_gather(ring, j, px, py, pz);
     const float dx = q.x - px, dy = q.y - py, dz = q.z - pz;
-    wd[s] = sqrt_rn(sqsum_1d(dx, dy, dz));
+    wd[s] = BIG ? sqrt_rn_big(sqsum_1d(dx, dy, dz)) : sqrt_rn(sqsum_1d(dx, dy, dz));
     wj[s] = j;
     nd[3 * s] = dx; nd[3 * s + 1] = dy; nd[3 * s + 2] = dz;  // the obs row's neighbour columns
   }
@@ -1610,7 +1645,8 @@ __device__ __forceinline__ uint32_t s64_finish_fast(const uint32_t (&nk)[KS], co
   for (int s = 0; s < MS; ++s) {
     const int j = (int)(ok[s] & oim);
     const float4 q = lds_f4(obst + (j & (S64_MMAX - 1)));
-    od[s] = sqrt_rn(sqsum_f(q.x - px, q.y - py, q.z - pz));
+    const float so = sqsum_f(q.x - px, q.y - py, q.z - pz);
+    od[s] = BIG ? sqrt_rn_big(so) : sqrt_rn(so);
     oj[s] = j;
   }
   od[MS] = __builtin_inff();
@@ -1979,8 +2015,19 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     }
   };
   auto select_topk = [&](bool dkey) {
-    const uint32_t fflags = s64_finish_fast<KS, MSL>(nk, ok, ring, obst, t, M, A->P.nb_keep, A->P.ob_keep, dkey, px, py,
-                                                     pz, wd, wj, od, oj, nd);
+    uint32_t fflags;
+    // the nearest keys bound every survivor's squared distance from below: a d~ key >= 2^-47 (or
+    // an s' key >= 2^-94; s' and d~ within 2^-20 of exact) and an exact obstacle key >= 2^-95 put
+    // every exact s the finish takes the square root of above sqrt_rn's 2^-96 slow-path limit
+    const bool big = SWARM_S64_BIGSQRT &&
+                     __ballot(!(__uint_as_float(nk[0] & A->P.nb_keep) >= (dkey ? 0x1p-47f : 0x1p-94f) &&
+                                __uint_as_float(ok[0] & A->P.ob_keep) >= 0x1p-95f)) == 0;
+    if (big)
+      fflags = s64_finish_fast<KS, MSL, true>(nk, ok, ring, obst, t, M, A->P.nb_keep, A->P.ob_keep, dkey, px, py, pz,
+                                              wd, wj, od, oj, nd);
+    else
+      fflags = s64_finish_fast<KS, MSL>(nk, ok, ring, obst, t, M, A->P.nb_keep, A->P.ob_keep, dkey, px, py, pz, wd,
+                                        wj, od, oj, nd);
     const uint64_t fails = __ballot(fflags != 0);
     if (fails == 0) return;
     bool slow_nb, slow_ob;
@@ -3263,8 +3310,9 @@ struct H256WLds {
   union {
     struct {
       double dsum[H_N];          // the secondary's own formation sums
-      float sum[2][H_N];         // mirror sums: [0] from block (b - 1, b), [1] from (b - 2, b)
-      float mn[3][H_N];          // mirror minima [0], [1]; the secondary's own minima [2]
+      float sum[3][H_N];         // mirror sums: [0] from block (b - 1, b), [1] from (b - 2, b), [2] the
+                                 // primary's share of (b - 1, b) (SWARM_S256W_SPLIT1)
+      float mn[4][H_N];          // mirror minima [0], [1]; the secondary's own minima [2]; [3] as sum[2]
     } p1;
     uint32_t keys[3][4][H_N];  // mirror lists [0] (b - 1, b), [1] (b - 2, b); the secondary's own [2]
   } x;
@@ -3556,6 +3604,13 @@ __device__ __forceinline__ s64_lds_cf* hw_base(H256WLds& L, int b, int t) {
 
 // The wide kernel's halves of h_pass1 / h_pass0.  Primary: block (w, w) and half of (w, w + 2);
 // secondary: block (w, w + 1), its own side into fsum / smin / nk, the mirror into set [0].
+// SWARM_S256W_SPLIT1 = S > 0: the formation pass's rotations S - 1 .. 0 of block (w, w + 1) move to
+// the primary (mirror set [2] / [3]); the secondary's travelled values, which stop at rotation S,
+// are rotated the remaining S lanes by one ds_bpermute each.
+#ifndef SWARM_S256W_SPLIT1
+#define SWARM_S256W_SPLIT1 0
+#endif
+static_assert(SWARM_S256W_SPLIT1 % 2 == 0 && SWARM_S256W_SPLIT1 < 64, "split on the two-copy rotation pairs");
 template <bool FAST, bool PRIMARY>
 __device__ __forceinline__ void hw_pass1(H256WLds& L, int w, int t, bool self, float px, float py, float pz, float ds,
                                          double& fsum, float& smin) {
@@ -3580,10 +3635,24 @@ __device__ __forceinline__ void hw_pass1(H256WLds& L, int w, int t, bool self, f
     }
     L.x.p1.sum[1][64 * b2 + t] = tc;
     L.x.p1.mn[1][64 * b2 + t] = __uint_as_float(tcm);
+    if constexpr (SWARM_S256W_SPLIT1 > 0) {
+      float tb = 0.f;
+      uint32_t tbm = 0x7f800000u;
+      h_seg1<FAST, SWARM_S256W_SPLIT1 - 1, 0, true, H_PS, 0>(hw_base<0>(L, b1, t), none, self, px, py, pz, ds, fsum,
+                                                              smin, tb, tbm);
+      L.x.p1.sum[2][64 * b1 + t] = tb;
+      L.x.p1.mn[3][64 * b1 + t] = __uint_as_float(tbm);
+    }
   } else {
     float tb = 0.f;
     uint32_t tbm = 0x7f800000u;
-    h_seg1<FAST, 63, 0, true, H_PS, 0>(hw_base<0>(L, b1, t), none, self, px, py, pz, ds, fsum, smin, tb, tbm);
+    h_seg1<FAST, 63, SWARM_S256W_SPLIT1, true, H_PS, 0>(hw_base<0>(L, b1, t), none, self, px, py, pz, ds, fsum, smin,
+                                                         tb, tbm);
+    if constexpr (SWARM_S256W_SPLIT1 > 0) {  // the travelled values' last S lanes
+      const int src = (int)((((uint32_t)t - SWARM_S256W_SPLIT1) & 63u) << 2);
+      tb = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(tb)));
+      tbm = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)tbm);
+    }
     L.x.p1.sum[0][64 * b1 + t] = tb;
     L.x.p1.mn[0][64 * b1 + t] = __uint_as_float(tbm);
     L.x.p1.dsum[64 * w + t] = fsum;
@@ -3983,6 +4052,12 @@ swarm_step256w(const S64Args args) {
   const int n_active = __syncthreads_count(act);
   STAMP256(1);
   A = s64_args();
+  // SWARM_S256W_PRIO: issue priority of the secondary over the (older) primary that shares its
+  // SIMD: 1 = during the formation pass, 2 = from here on (the oldest wave issues first otherwise)
+#ifndef SWARM_S256W_PRIO
+#define SWARM_S256W_PRIO 0
+#endif
+  if (SWARM_S256W_PRIO == 2 && !primary) __builtin_amdgcn_s_setprio(1);
 
   // ---- integrate: drone_swarm_env.py:98-117 (swarm_kernel, DYN_KIN)
   float prev_d = 0.f;
@@ -4034,8 +4109,10 @@ swarm_step256w(const S64Args args) {
   } else {
     const float qx = L.seg2[w][0][t], qy = L.seg2[w][1][t], qz = L.seg2[w][2][t];
     const bool self = L.seg2[w][3][t] != 0.f;
+    if (SWARM_S256W_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     if (fast) hw_pass1<true, false>(L, w, t, true, qx, qy, qz, A->P.ds_f, fsum, smin);
     else hw_pass1<false, false>(L, w, t, self, qx, qy, qz, A->P.ds_f, fsum, smin);
+    if (SWARM_S256W_PRIO == 1) __builtin_amdgcn_s_setprio(0);
   }
   STAMP256(3);
   __syncthreads();  // handed-over sums / minima written
@@ -4044,6 +4121,10 @@ swarm_step256w(const S64Args args) {
     fsum += (double)L.x.p1.sum[0][i];
     fsum += (double)L.x.p1.sum[1][i];
     smin = fminf(fminf(smin, L.x.p1.mn[2][i]), fminf(L.x.p1.mn[0][i], L.x.p1.mn[1][i]));
+    if constexpr (SWARM_S256W_SPLIT1 > 0) {
+      fsum += (double)L.x.p1.sum[2][i];
+      smin = fminf(smin, L.x.p1.mn[3][i]);
+    }
   }
   A = s64_args();
 
@@ -4214,8 +4295,19 @@ swarm_step256w(const S64Args args) {
   }
   A = s64_args();
 
-  // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)], straight from registers
-  float* row = A->O.obs + ag * (9 + 4 * H_K + 4 * H_MS);
+  // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)]
+  constexpr int D = 9 + 4 * H_K + 4 * H_MS;
+#ifndef SWARM_S256W_STAGE
+#define SWARM_S256W_STAGE 0
+#endif
+#if SWARM_S256W_STAGE
+  // staged like step64's rows: 16 rows at a time in this wave's (dead) plane segment, then stored
+  // as coalesced 16-B write-through buffer stores of the wave's contiguous 64-row block — straight
+  // from registers, every dword store touched 64 lines (148-B row stride), partial-line writes
+  float row[D];
+#else
+  float* row = A->O.obs + ag * D;  // straight from registers
+#endif
   row[0] = px; row[1] = py; row[2] = pz;
   row[3] = vx; row[4] = vy; row[5] = vz;
   row[6] = gx - px; row[7] = gy - py; row[8] = gz - pz;
@@ -4229,6 +4321,33 @@ swarm_step256w(const S64Args args) {
     const float4 q = lds_f4(L.obst + (oj[s] & (H_MMAX - 1)));
     row[21 + 4 * s] = q.x - px; row[22 + 4 * s] = q.y - py; row[23 + 4 * s] = q.z - pz; row[24 + 4 * s] = od[s];
   }
+#if SWARM_S256W_STAGE
+  {
+    constexpr int CH = 16, V4 = CH * D / 4, NF = V4 / 64, NR = V4 % 64;
+    static_assert(CH * D <= 4 * H_PS && (CH * D) % 4 == 0 && H_N % CH == 0, "stage chunk in the wave's planes");
+    // this wave's planes are dead: every pass-0 read precedes the hand-over barrier
+    float* stage = &L.seg2[w][0][0];
+    const float4* s4 = reinterpret_cast<const float4*>(stage);
+    float* srow = stage + (t % CH) * D;
+    float* const ob = A->O.obs + ((size_t)env * H_N + 64 * w) * D;  // the wave's 64 rows, contiguous
+#pragma unroll
+    for (int ch = 0; ch < 64 / CH; ++ch) {
+      if (t / CH == ch) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) srow[k] = row[k];
+      }
+      wave_sync();
+      float4 v[NF + 1];
+#pragma unroll
+      for (int k = 0; k < NF; ++k) v[k] = s4[t + 64 * k];
+      if (NR && t < NR) v[NF] = s4[t + 64 * NF];
+#pragma unroll
+      for (int k = 0; k < NF; ++k) store_obs(ob, 64 * D * 4, 16u * (ch * V4 + t + 64 * k), v[k]);
+      if (NR && t < NR) store_obs(ob, 64 * D * 4, 16u * (ch * V4 + t + 64 * NF), v[NF]);
+      wave_sync();
+    }
+  }
+#endif
   STAMP256(8);
   STAMP_END(env, threadIdx.x == 0);
 }
@@ -4681,7 +4800,8 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
     if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SWARM_OK;
   }
-  if (mode == MODE_STEP && step256_applies(p, kp) && !s->env_cfg) {
+  // (16-B aligned obs: the wide kernel stages its rows and stores them as 16-B buffer stores)
+  if (mode == MODE_STEP && step256_applies(p, kp) && !s->env_cfg && ((uintptr_t)o->obs) % 16 == 0) {
     const S64Args args{kp, *s, actions, amask, *o};
     int threads = 0, lds = 0;
     const step64_fn k256 = reinterpret_cast<step64_fn>(swarm_pick_step256(&threads, &lds));

@@ -46,11 +46,11 @@ def _snap(vec):
 def test_uniform_records_equal_no_records(dev, n, e, dyn, groups):
     from swarm_marl_amd import VecSwarm
     cfg = {"num_drones": n, "max_steps": 7}
-    # N = 16 / 256 without records run swarm_step16q / swarm_step256w, whose rewards equal the
-    # generic kernel's within 1e-5 only (formation partial sums in another order;
-    # tests/test_gpu_step16.py, test_gpu_step256.py): compare the records path with the generic
-    # kernel there
-    kp = "generic" if n in (16, 256) else "auto"
+    # N = 16 / 64 / 256 without records run swarm_step16q / swarm_step64_once / swarm_step256w, whose
+    # kinematic rewards equal the generic kernel's within 1e-5 only (formation partial sums in
+    # another order; tests/test_gpu_step16.py, test_gpu_step64.py, test_gpu_step256.py): compare
+    # the records path with the generic kernel there
+    kp = "generic" if n in (16, 64, 256) and dyn == "kinematic" else "auto"
     a_vec = VecSwarm(e, cfg, device=dev, auto_reset=True, seed=11, dynamics=dyn, groups=groups, kernel_path=kp)
     b_vec = VecSwarm(e, cfg, device=dev, auto_reset=True, seed=11, dynamics=dyn, groups=groups)
     b_vec.set_env_config()  # records holding the batch config

@@ -1,7 +1,7 @@
 """GPU: the headline specialisation swarm_step64 (N = 64, K = 3, Ms = 4, 4 <= M <= 16, kinematic)
 against the generic swarm_kernel (kernel_path="generic") on identical inputs — every output and
-every state tensor bit-identical, step after step with in-kernel auto-reset — and against the CPU
-oracle.  The golden-fixture / oracle tests of test_gpu_parity.py at N = 64 run through step64 too.
+every state tensor bit-identical (kinematic rewards within 1e-5: the formation sum's f32 chain),
+step after step with in-kernel auto-reset — and against the CPU oracle.  The golden-fixture / oracle tests of test_gpu_parity.py at N = 64 run through step64 too.
 """
 from __future__ import annotations
 
@@ -30,17 +30,24 @@ def _pair(dev, raw, e, **kw):
     return a, b
 
 
-OUTS = ("obs", "reward", "terminated", "truncated", "env_done", "dist_goal", "info_flags",
-        "global_state")
+OUTS = ("obs", "terminated", "truncated", "env_done", "dist_goal", "info_flags", "global_state")
 STATE = ("pos", "vel", "goal", "obstacles", "active", "step_count", "episode")
+# round 6: step64 sums a pass's formation terms in one f32 chain (the generic kernel widens every
+# 4-rotation group to f64), so kinematic rewards agree within the 1e-5 reward contract, not bit for
+# bit; everything else (and the physics rewards, which carry no formation term) stays bitwise
+REWARD_TOL = 1e-5
 
 
-def _assert_same(a, b, tag):
+def _assert_same(a, b, tag, reward_exact=False):
     for name in OUTS + STATE:
         x, y = getattr(a, name), getattr(b, name)
         if not torch.equal(x, y):
             bad = (x != y).nonzero()[:5].tolist()
             raise AssertionError(f"{tag}: {name} differs at {bad}")
+    if reward_exact:
+        assert torch.equal(a.reward, b.reward), f"{tag}: reward differs"
+    err = (a.reward.double() - b.reward.double()).abs().max().item()
+    assert err <= REWARD_TOL, f"{tag}: reward err {err}"
 
 
 def test_kernel_selection():
@@ -203,7 +210,7 @@ def test_step64_physics_matches_generic(dev, m, max_steps, masked, law):
         am = (torch.rand((e, 64), device=dev, generator=g) > 0.1) if masked else None
         a.step(act, am)
         b.step(act, am)
-        _assert_same(a, b, f"physics t={t}")
+        _assert_same(a, b, f"physics t={t}", reward_exact=True)
         assert torch.equal(a.damping, b.damping), f"physics t={t}: damping"
         resets += int(((a.env_done & 4) != 0).sum())
     assert resets > 0
