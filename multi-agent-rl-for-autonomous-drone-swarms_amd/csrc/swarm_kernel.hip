@@ -3750,16 +3750,17 @@ __device__ __forceinline__ uint32_t h_finish_fast(const uint32_t (&nk)[4], const
 #if SWARM_HAS_PART(7)  // emitted in its own translation unit only
 }  // namespace swarm_dev
 namespace {  // kernels: internal to this translation unit
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) swarm_step256(const S64Args args) {
-  (void)args;  // read through s64_args()
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) swarm_step256(S64_ONCE_PARAMS) {
+  // (the leading arguments of the wide kernel's launch, unused here: everything from the args block)
+  (void)pos; (void)vel; (void)actions; (void)active; (void)goal; (void)amask; (void)E;  // M: the launch's obstacle count
+  (void)args;  // read through s64_args<S64_HOT_BYTES>()
   constexpr int KS = H_K + 1, MSL = H_MS + 1;
   __shared__ H256Lds L;
   const int i = threadIdx.x;  // drone
   const int w = __builtin_amdgcn_readfirstlane(i >> 6), t = i & 63;
-  S64ArgPtr A = s64_args();
+  S64ArgPtr A = s64_args<S64_HOT_BYTES>();
   const int env = blockIdx.x;
   if (env >= A->P.E) return;  // whole block
-  const int M = A->P.M;
   const size_t ag = (size_t)env * H_N + i;
   STAMP256(0);
   STAMP_BEGIN(env, i == 0);
@@ -3782,7 +3783,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   float gx = gx0, gy = gy0, gz = gz0;
   const int n_active = __syncthreads_count(act);
   STAMP256(1);
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
 
   // ---- integrate: drone_swarm_env.py:98-117 (swarm_kernel, DYN_KIN)
   float prev_d = 0.f;
@@ -3816,7 +3817,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   h_put(L, w, t, px, py, pz, act ? 1.f : 0.f);
   const bool fast = __syncthreads_and(act) != 0;  // also the barrier after the puts
   STAMP256(2);
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
 
   // ---- formation + minimum pass (every pair once), obstacle pass
   double fsum = 0.0;
@@ -3833,7 +3834,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   fsum += (double)L.x.p1.sum[0][i];
   fsum += (double)L.x.p1.sum[1][i];
   smin = fminf(smin, fminf(L.x.p1.mn[0][i], L.x.p1.mn[1][i]));
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
 
   STAMP256(4);
   // ---- rewards / terminations: drone_swarm_env.py:120-172 (swarm_kernel, DYN_KIN)
@@ -3865,7 +3866,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   __syncthreads();
   const uint32_t votes = L.red[0] | L.red[1] | L.red[2] | L.red[3];
   const bool any_c = (votes & 1u) != 0, any_cand = (votes & 2u) != 0;
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
   if (n_active == 0) {
     term_all = true;
   } else {
@@ -3928,7 +3929,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     obstacle_pass_s64<MSL, false>(L.osoa, M, px, py, pz, false, 0.f, A->P.ob_keep, ok, c2);
   }
   STAMP256(6);
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
   uint32_t nk[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
@@ -3943,7 +3944,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
 #pragma unroll
     for (int s = 0; s < KS; ++s) nk[s] = h_decode(nk[s], w, t, A->P.nb_keep);
   }
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
 
   // ---- exact top-K of the emitted observation (keys rank by s', drone indices)
   float wd[KS], od[MSL];
@@ -3959,7 +3960,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     }
   }
   STAMP256(7);
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
 
   // ---- state write-back
   const bool new_act = do_reset || cont;
@@ -3984,7 +3985,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     gs[3 * H_N + 3 * i] = vx; gs[3 * H_N + 3 * i + 1] = vy; gs[3 * H_N + 3 * i + 2] = vz;
     if (i == 0) { gs[6 * H_N] = gx; gs[6 * H_N + 1] = gy; gs[6 * H_N + 2] = gz; }
   }
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
 
   // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)], straight from registers
   float* row = A->O.obs + ag * (9 + 4 * H_K + 4 * H_MS);
@@ -4014,36 +4015,44 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
 #define SWARM_S256W_WAVES 6  // 80 VGPRs: three 512-thread workgroups per CU
 #endif
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SWARM_S256W_WAVES)))
-swarm_step256w(const S64Args args) {
-  (void)args;  // read through s64_args()
+swarm_step256w(S64_ONCE_PARAMS) {
+  (void)args;  // read through s64_args<S64_HOT_BYTES>()
+  // the leading arguments (preloaded into SGPRs, -amdgpu-kernarg-preload-count=16 for this unit):
+  // the bound test and the primary's first loads issue without a scalar load of the kernarg segment
+  const S64Hot H = S64_ONCE_HOT;
   constexpr int KS = H_K + 1, MSL = H_MS + 1;
   __shared__ H256WLds L;
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const bool primary = wv < 4;
   const int w = wv & 3, t = threadIdx.x & 63;
   const int i = 64 * w + t;  // drone
-  S64ArgPtr A = s64_args();
   const int env = blockIdx.x;
-  if (env >= A->P.E) return;  // whole block
-  const int M = A->P.M;
+  if (env >= H.E) return;  // whole block
   const size_t ag = (size_t)env * H_N + i;
   STAMP256(0);
   STAMP_BEGIN(env, threadIdx.x == 0);
 
-  // ---- loads (the secondary: obstacles)
-  const int stepc = A->S.step_count[env];
-  const uint32_t episode0 = A->S.episode[env];
+  // ---- loads (the secondary: obstacles); 32-bit element offsets (step256_applies: E x 256 x 3 < 2^32)
   float gx = 0.f, gy = 0.f, gz = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
   float px = 0.f, py = 0.f, pz = 0.f, vx = 0.f, vy = 0.f, vz = 0.f;
   bool act = false, has = true;
   if (primary) {
-    gx = A->S.goal[3 * env]; gy = A->S.goal[3 * env + 1]; gz = A->S.goal[3 * env + 2];
-    ax = A->actions[ag * 3]; ay = A->actions[ag * 3 + 1]; az = A->actions[ag * 3 + 2];
-    px = A->S.pos[ag * 3]; py = A->S.pos[ag * 3 + 1]; pz = A->S.pos[ag * 3 + 2];
-    vx = A->S.vel[ag * 3]; vy = A->S.vel[ag * 3 + 1]; vz = A->S.vel[ag * 3 + 2];
-    act = A->S.active[ag] != 0;
-    has = A->amask == nullptr || A->amask[ag] != 0;
-  } else if (i < M) {
+    // wave-uniform row bases (SGPRs) + 32-bit lane offsets: saddr-form loads, no 64-bit lane math
+    const uint32_t wb = (uint32_t)env * H_N + 64u * (uint32_t)w, t3 = 3u * (uint32_t)t, g3 = 3u * (uint32_t)env;
+    const float* __restrict__ pe = H.pos + 3u * wb;
+    const float* __restrict__ ve = H.vel + 3u * wb;
+    const float* __restrict__ ae = H.actions + 3u * wb;
+    gx = __uint_as_float(H.goal[g3]); gy = __uint_as_float(H.goal[g3 + 1]); gz = __uint_as_float(H.goal[g3 + 2]);
+    ax = ae[t3]; ay = ae[t3 + 1]; az = ae[t3 + 2];
+    px = pe[t3]; py = pe[t3 + 1]; pz = pe[t3 + 2];
+    vx = ve[t3]; vy = ve[t3 + 1]; vz = ve[t3 + 2];
+    act = (H.active + wb)[t] != 0;
+    has = H.amask == nullptr || (H.amask + wb)[t] != 0;
+  }
+  S64ArgPtr A = s64_args<S64_HOT_BYTES>();
+  const int stepc = A->S.step_count[env];
+  const uint32_t episode0 = A->S.episode[env];
+  if (!primary && i < M) {
     const float* o = A->S.obstacles + ((size_t)env * M + i) * 3;
     const float ox = o[0], oy = o[1], oz = o[2];
     L.obst[i] = make_float4(ox, oy, oz, 0.f);
@@ -4051,7 +4060,7 @@ swarm_step256w(const S64Args args) {
   }
   const int n_active = __syncthreads_count(act);
   STAMP256(1);
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
   // SWARM_S256W_PRIO: issue priority of the secondary over the (older) primary that shares its
   // SIMD: 1 = during the formation pass, 2 = from here on (the oldest wave issues first otherwise)
 #ifndef SWARM_S256W_PRIO
@@ -4093,7 +4102,7 @@ swarm_step256w(const S64Args args) {
   }
   const bool fast = __syncthreads_and(act || !primary) != 0;  // also the barrier after the puts
   STAMP256(2);
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
 
   // ---- formation + minimum pass (every pair once, split over the two waves), obstacle pass
   double fsum = 0.0;
@@ -4126,7 +4135,7 @@ swarm_step256w(const S64Args args) {
       smin = fminf(smin, L.x.p1.mn[3][i]);
     }
   }
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
 
   STAMP256(4);
   // ---- rewards / terminations: drone_swarm_env.py:120-172 (swarm_kernel, DYN_KIN)
@@ -4157,7 +4166,7 @@ swarm_step256w(const S64Args args) {
   __syncthreads();
   const uint32_t votes = L.red[0] | L.red[1] | L.red[2] | L.red[3];
   const bool any_c = (votes & 1u) != 0, any_cand = (votes & 2u) != 0;
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
   if (n_active == 0) {
     term_all = true;
   } else {
@@ -4231,7 +4240,7 @@ swarm_step256w(const S64Args args) {
     }
   }
   STAMP256(6);
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
   uint32_t nk[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) nk[s] = KEY_EMPTY;
@@ -4257,7 +4266,7 @@ swarm_step256w(const S64Args args) {
 #pragma unroll
     for (int s = 0; s < KS; ++s) nk[s] = h_decode(nk[s], w, t, A->P.nb_keep);
   }
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
 
   // ---- exact top-K of the emitted observation (keys rank by s', drone indices)
   float wd[KS], od[MSL];
@@ -4273,7 +4282,7 @@ swarm_step256w(const S64Args args) {
     }
   }
   STAMP256(7);
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
 
   // ---- state write-back
   const bool new_act = do_reset || cont;
@@ -4293,12 +4302,12 @@ swarm_step256w(const S64Args args) {
     gs[3 * H_N + 3 * i] = vx; gs[3 * H_N + 3 * i + 1] = vy; gs[3 * H_N + 3 * i + 2] = vz;
     if (i == 0) { gs[6 * H_N] = gx; gs[6 * H_N + 1] = gy; gs[6 * H_N + 2] = gz; }
   }
-  A = s64_args();
+  A = s64_args<S64_HOT_BYTES>();
 
   // ---- observation row [p | v | g-p | K x (p_j-p, d) | Ms x (o_m-p, d)]
   constexpr int D = 9 + 4 * H_K + 4 * H_MS;
 #ifndef SWARM_S256W_STAGE
-#define SWARM_S256W_STAGE 0
+#define SWARM_S256W_STAGE 1  // r06c: 36.68 / 36.88 / 37.24 vs 38.10 / 38.21 / 38.58 us (config 5, graph, 4 groups)
 #endif
 #if SWARM_S256W_STAGE
   // staged like step64's rows: 16 rows at a time in this wave's (dead) plane segment, then stored
@@ -4536,7 +4545,7 @@ bool step16q_applies(const swarm_params_t* p, const KParams& k) {
 // The config-5 specialisation swarm_step256 covers N = 256, K = 3, Ms = 4, 4 <= M <= 16, kinematic.
 bool step256_applies(const swarm_params_t* p, const KParams& k) {
   return p->kernel_path == SWARM_PATH_AUTO && k.N == H_N && k.K == H_K && k.Ms == H_MS && k.M >= H_MS &&
-         k.M <= H_MMAX && p->dynamics == DYN_KIN;
+         k.M <= H_MMAX && k.E <= SPEC_MAX_E && p->dynamics == DYN_KIN;  // E x 256 x 3 < 2^32: 32-bit offsets
 }
 
 // Persistent grid of swarm_step64: waves_per_simd x 4 SIMDs x the current device's CUs (E when
@@ -4804,8 +4813,11 @@ int launch(int mode, const swarm_params_t* p, const swarm_state_t* s, const floa
   if (mode == MODE_STEP && step256_applies(p, kp) && !s->env_cfg && ((uintptr_t)o->obs) % 16 == 0) {
     const S64Args args{kp, *s, actions, amask, *o};
     int threads = 0, lds = 0;
-    const step64_fn k256 = reinterpret_cast<step64_fn>(swarm_pick_step256(&threads, &lds));
-    hipLaunchKernelGGL(k256, dim3(kp.E), dim3(threads), 0, (hipStream_t)stream, args);
+    // the first loads' addresses, E and M lead the arguments (preloaded into SGPRs, as step64 / step16q)
+    const step64o_fn k256 = reinterpret_cast<step64o_fn>(swarm_pick_step256(&threads, &lds));
+    hipLaunchKernelGGL(k256, dim3(kp.E), dim3(threads), 0, (hipStream_t)stream, (const float*)s->pos,
+                       (const float*)s->vel, actions, (const uint8_t*)s->active, (const uint32_t*)s->goal, amask, kp.E,
+                       kp.M, args);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(SWARM_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SWARM_OK;

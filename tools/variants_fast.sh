@@ -12,8 +12,8 @@ for spec in "$@"; do
   name=${spec%%:*}; rest=${spec#*:}; unit=${rest%%:*}; flags=${rest#*:}; flags=${flags//,/ }
   case $unit in
     part*) src=$C/swarm_kernel.hip; defs="-DSWARM_PART=${unit#part}"; base=swarm_kernel.$unit.o
-           # the product's per-part flags (__graft_entry__.PART_FLAGS): kernarg preload for parts 5, 6
-           case $unit in part5|part6) defs="$defs -mllvm -amdgpu-kernarg-preload-count=16" ;; esac ;;
+           # the product's per-part flags (__graft_entry__.PART_FLAGS): kernarg preload for parts 5, 6, 7
+           case $unit in part5|part6|part7) defs="$defs -mllvm -amdgpu-kernarg-preload-count=16" ;; esac ;;
     policy) src=$C/swarm_policy.hip; defs=""; base=swarm_policy.o ;;
     eval) src=$C/swarm_eval.hip; defs=""; base=swarm_eval.o ;;
     *) echo "unknown unit $unit"; exit 2 ;;
