@@ -1369,6 +1369,30 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// XCD-aware workgroup order: the dispatcher places workgroup b on XCD b mod 8 (round robin), and
+// each XCD's L2 fetches a line that two envs share (rows that are not 128-B multiples: step16q's
+// 192-B position rows, every kernel's active bytes, goals, obstacles) once for each XCD that
+// touches it.  The bijection below hands XCD x a contiguous block of workgroup slots, so
+// neighbouring envs share an XCD and their shared lines are fetched once (r06e: TCC_EA0_RDREQ
+// counts one 128-B request per line and XCD, tools/rdreq_probe.hip).  Envs are independent: the
+// order never changes a result.
+// Measured (r06f, three alternating pairs each): config 2 (step16q) 5.42-5.45 vs 5.74-5.75 us and reads
+// 1.60 -> 1.05 MB; config 5 (step256w) 35.98-36.17 vs 36.16-36.50 us; the headline (step64_once,
+// whose rows are whole lines: only active bytes, goals and obstacles are shared) within the spread
+// (driver command 24.0-25.0 vs 23.8-24.4 us), so step64 keeps the dispatch order (SWARM_S64_XCD_MAP).
+#ifndef SWARM_XCD_MAP
+#define SWARM_XCD_MAP 1
+#endif
+#ifndef SWARM_S64_XCD_MAP
+#define SWARM_S64_XCD_MAP 0
+#endif
+template <bool ON = SWARM_XCD_MAP != 0>
+__device__ __forceinline__ int xcd_slot(int b, int nb) {
+  if (!ON) return b;
+  const int q = nb >> 3, r = nb & 7, x = b & 7, k = b >> 3;
+  return x * q + (x < r ? x : r) + k;
+}
+
 // A wave's LDS: positions + obstacles during the step, the obs staging chunk afterwards.
 // Positions are held twice: `ring` (float4 per drone, for the exact finish and the obs row) and
 // the pair-pass ring as structure-of-arrays `soa` (x, y, z, eligibility planes of S64_SOA
@@ -2464,7 +2488,7 @@ __device__ __forceinline__ void s64_once_body(const S64Hot& H) {
   __shared__ S64Lds<CH> lds[G];
   const int t = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int env = blockIdx.x * G + w;
+  const int env = xcd_slot<SWARM_S64_XCD_MAP != 0>((int)blockIdx.x, (int)gridDim.x) * G + w;
   if (env >= H.E) return;  // whole wave (the last workgroup of a ragged E)
   S64In cur;
   s64_load<DYN>(s64_args<S64_HOT_BYTES>(), H, env, t, cur);
@@ -3089,7 +3113,7 @@ swarm_step16q(const float* __restrict__ pos, const float* __restrict__ vel, cons
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   S64ArgPtr A = q16_args();
   const Q16Hot H{pos, vel, actions, active, goal, step_count, amask};
-  const int env = blockIdx.x;  // grid = E
+  const int env = xcd_slot((int)blockIdx.x, (int)gridDim.x);  // grid = E
   // the step's waves (the launch's critical path) issue ahead of the next-episode waves sharing
   // their SIMDs: 5.82-5.84 -> 5.71-5.73 us per step (priority 3 no better, r05aa)
   if (wv != 2) __builtin_amdgcn_s_setprio(1);
@@ -3608,7 +3632,8 @@ __device__ __forceinline__ s64_lds_cf* hw_base(H256WLds& L, int b, int t) {
 // the primary (mirror set [2] / [3]); the secondary's travelled values, which stop at rotation S,
 // are rotated the remaining S lanes by one ds_bpermute each.
 #ifndef SWARM_S256W_SPLIT1
-#define SWARM_S256W_SPLIT1 0
+#define SWARM_S256W_SPLIT1 16  // r06d / r06e: 36.07 / 35.81 / 36.03, 36.22 / 35.92 / 36.12 vs 35.97 / 36.41 / 36.37,
+                               // 36.40 / 36.28 / 36.10 us (5 of 6 pairs); the primary's hand-over wait 4.9k -> 2.0k cycles
 #endif
 static_assert(SWARM_S256W_SPLIT1 % 2 == 0 && SWARM_S256W_SPLIT1 < 64, "split on the two-copy rotation pairs");
 template <bool FAST, bool PRIMARY>
@@ -4026,7 +4051,7 @@ swarm_step256w(S64_ONCE_PARAMS) {
   const bool primary = wv < 4;
   const int w = wv & 3, t = threadIdx.x & 63;
   const int i = 64 * w + t;  // drone
-  const int env = blockIdx.x;
+  const int env = xcd_slot((int)blockIdx.x, (int)gridDim.x);
   if (env >= H.E) return;  // whole block
   const size_t ag = (size_t)env * H_N + i;
   STAMP256(0);
