@@ -77,7 +77,8 @@ def fold(rnd: str) -> None:
         cs = acc[ks[0]]
         mean = {c: (sum(v[len(v) // 4:]) / len(v[len(v) // 4:]) if len(v) > 8 else sum(v) / len(v))
                 for c, v in cs.items()}
-        out.append({"config": cfg, "kernel": kname, **{c: round(x, 1) for c, x in sorted(mean.items())}})
+        kfull = ks[0].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+        out.append({"config": cfg, "kernel": kfull, **{c: round(x, 1) for c, x in sorted(mean.items())}})
     f = ROOT / "profiles" / f"{rnd}_valu_class_pmc.jsonl"
     f.write_text("".join(json.dumps(r) + "\n" for r in out))
     print(f"wrote {f} ({len(out)} configs)")
@@ -100,7 +101,8 @@ def table(rnd: str, record: bool = False) -> None:
         lo = sum(n * price[c][0] for c, n in counts.items()) / waves  # ns per wave (SIMD issue time)
         hi = sum(n * price[c][1] for c, n in counts.items()) / waves
         wps = waves / simds
-        print(f"\n{cfg}: {kname}, {waves:.0f} waves per dispatch ({wps:.1f} per SIMD), {total / waves:.0f} VALU per wave")
+        print(f"\n{cfg}: {r.get('kernel', kname)}, {waves:.0f} waves per dispatch ({wps:.1f} per SIMD), "
+              f"{total / waves:.0f} VALU per wave")
         for c, n in counts.items():
             print(f"  {c:26s} {n / waves:7.1f} per wave   {price[c][0]:.3f}-{price[c][1]:.3f} ns")
         print(f"  VALU issue time per SIMD per dispatch: {lo * wps * 1e-3:.1f} - {hi * wps * 1e-3:.1f} us "
