@@ -769,9 +769,15 @@ def main(argv=None):
             roof["valu"] = valu_roofline(prof, kern_max)
             busy = roof["valu"].get("busy_frac")
             if busy is not None and busy > roof["frac"]:
-                roof["bound"] = "valu"
-                roof["bound_note"] = ("the SIMDs' VALU issue (roofline.valu.busy_frac, class-costed) is busier "
-                                      "than HBM (frac); achieved / peak / unit / frac stay the HBM figures")
+                if busy >= 0.5:
+                    roof["bound"] = "valu"
+                    roof["bound_note"] = ("the SIMDs' VALU issue (roofline.valu.busy_frac, class-costed) is busier "
+                                          "than HBM (frac); achieved / peak / unit / frac stay the HBM figures")
+                else:  # config 2: one to three waves per SIMD, the serial path of a wave sets the step
+                    roof["bound"] = "latency"
+                    roof["bound_note"] = ("neither the VALU issue (roofline.valu.busy_frac) nor HBM (frac) is half "
+                                          "busy: the launch is latency-bound; achieved / peak / unit / frac stay the "
+                                          "HBM figures")
         metric = METRIC if pol is None else \
             "rollout agent-steps/sec (on-device policy + env step) at N=64 x E=8192 per MI355X"
         if tracker is not None:
