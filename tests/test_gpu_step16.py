@@ -218,3 +218,22 @@ def test_step16q_goal_radius_boundary(dev, radius):
     _assert_same(a, b, f"goal boundary r={radius}")
     reached = (a.info_flags.cpu().numpy() & 2) != 0
     assert 0 < reached.sum() < reached.size  # the boundary runs through the sample
+
+
+@pytest.mark.parametrize("e,groups", [(1, 1), (7, 1), (1001, 3)])
+def test_step16q_xcd_order_ragged_and_groups(dev, e, groups):
+    """The XCD-aware workgroup order (round 6: XCD x takes a contiguous block of envs) on grids that
+    are not multiples of 8 and on env groups of unequal size launched on their own streams: every env
+    is stepped exactly once, as by the generic kernel."""
+    raw = dict(num_drones=16, max_steps=6)
+    a, b = _pair(dev, raw, e, auto_reset=True, seed=23, groups=groups)
+    assert a.kernel_name() == "swarm_step16q"
+    a.reset()
+    b.reset()
+    g = torch.Generator(device=dev).manual_seed(29)
+    for t in range(8):
+        act = torch.rand((e, 16, 3), device=dev, generator=g) * 2 - 1
+        a.step(act)
+        b.step(act)
+        torch.cuda.synchronize()
+        _assert_same(a, b, f"E={e} groups={groups} t={t}")
