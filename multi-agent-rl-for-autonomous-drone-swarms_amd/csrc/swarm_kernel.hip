@@ -201,6 +201,28 @@ __device__ __forceinline__ float wave_ror1(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x13C, 0xF, 0xF, false));
 }
 
+// A missing agent's action is zero (drone_swarm_env.py:104): the three components ANDed with a lane
+// mask (one select + three full-rate v_and_b32).  `if (!has) a = 0` compiled to three e32 v_cndmask
+// reading VCC, and runs of those issue ~7 ns apart per SIMD against ~2 for the e64 form
+// (tools/valu_rate6.hip, profiles/r06d_valu_rate6.txt); the mask is opaque so the AND is not folded
+// back into the selects.  Bitwise the same values (+0 for a missing agent).  Off by default: three
+// same-box pairs each (profiles/r06k_act_mask_ab.jsonl) put the headline default command 0.1 us slower
+// with the mask and configs 2 / driver within noise; the run of three cndmasks sits once per wave
+// where the scheduler hides it.
+#ifndef SWARM_ACT_MASK
+#define SWARM_ACT_MASK 0
+#endif
+__device__ __forceinline__ void zero_unless(bool has, float& ax, float& ay, float& az) {
+  if constexpr (SWARM_ACT_MASK) {
+    uint32_t m = has ? 0xffffffffu : 0u;
+    asm volatile("" : "+v"(m));
+    ax = __uint_as_float(__float_as_uint(ax) & m);
+    ay = __uint_as_float(__float_as_uint(ay) & m);
+    az = __uint_as_float(__float_as_uint(az) & m);
+  } else if (!has) {
+    ax = 0.f; ay = 0.f; az = 0.f;
+  }
+}
 // np.clip of a float32 in [lo, hi] (lo <= hi): one v_med3_f32
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
 __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
@@ -1954,7 +1976,7 @@ __device__ __forceinline__ void s64_env(const int env, const int M, const S64In&
     }
   } else if (act) {
     prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
-    if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
+    zero_unless(has, ax, ay, az);
     ax = clampf(ax, -1.f, 1.f) * A->P.amax;
     ay = clampf(ay, -1.f, 1.f) * A->P.amax;
     az = clampf(az, -1.f, 1.f) * A->P.amax;
@@ -3016,7 +3038,7 @@ __device__ __forceinline__ void q16_integrate(S64ArgPtr A, const Q16Hot& H, int 
   float prev_d = 0.f;
   if (st.act) {
     prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
-    if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
+    zero_unless(has, ax, ay, az);
     ax = clampf(ax, -1.f, 1.f) * A->P.amax;
     ay = clampf(ay, -1.f, 1.f) * A->P.amax;
     az = clampf(az, -1.f, 1.f) * A->P.amax;
@@ -4098,7 +4120,7 @@ swarm_step256w(S64_ONCE_PARAMS) {
   if (primary) {
     if (act) {
       prev_d = sqrt_rn(sqsum_1d(gx - px, gy - py, gz - pz));
-      if (!has) { ax = 0.f; ay = 0.f; az = 0.f; }
+      zero_unless(has, ax, ay, az);
       ax = clampf(ax, -1.f, 1.f) * A->P.amax;
       ay = clampf(ay, -1.f, 1.f) * A->P.amax;
       az = clampf(az, -1.f, 1.f) * A->P.amax;
