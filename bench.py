@@ -201,12 +201,19 @@ def max_over_ranks(values, world: int, device=None) -> list[float]:
     return [float(x) for x in t.cpu()]
 
 
+def _barrier_on(world: int) -> bool:
+    if world > 1:
+        return True
+    import torch.distributed as dist
+    return os.environ.get("SWARM_BENCH_ONE_RANK_PG") == "1" and dist.is_initialized()
+
+
 def timed_region(body, world: int, sync, spin=None, pre=None) -> float:
     """Barrier + sync, run `body`, sync + barrier; wall seconds of this rank.  `spin`: an event
     polled until it completes before the closing sync (diagnostic --spin-sync).  `pre`: run
     before the opening sync (the start events of the device-time bracket: their host cost would
     otherwise delay the region's first launch)."""
-    if world > 1:
+    if _barrier_on(world):
         import torch.distributed as dist
         dist.barrier()
     if pre is not None:
@@ -218,7 +225,7 @@ def timed_region(body, world: int, sync, spin=None, pre=None) -> float:
         while not spin.query():
             pass
     sync()
-    if world > 1:
+    if _barrier_on(world):
         import torch.distributed as dist
         dist.barrier()
     return time.perf_counter() - t0
@@ -373,7 +380,12 @@ def main(argv=None):
     dev = torch.device("cuda", local if world > 1 and not rehearsal else 0)
     torch.cuda.set_device(dev)
     own_pg = False
-    if world == 1 and os.environ.get("SWARM_BENCH_FORCE_GATHER") == "1" and args.ctde and not dist.is_initialized():
+    # SWARM_BENCH_ONE_RANK_PG=1 (diagnostic): a one-rank RCCL group whose barrier brackets the timed
+    # region, so a one-GPU box sees the streams and queues a multi-rank process holds (the group
+    # count rule below parse(): profiles/r06l_groups_rccl_ab.jsonl)
+    one_rank_pg = world == 1 and os.environ.get("SWARM_BENCH_ONE_RANK_PG") == "1"
+    if world == 1 and (one_rank_pg or (os.environ.get("SWARM_BENCH_FORCE_GATHER") == "1" and args.ctde)) \
+            and not dist.is_initialized():
         # the CTDE gather on one GPU: a one-rank RCCL group (its cost on the step)
         import socket
         with socket.socket() as so_:
