@@ -17,7 +17,9 @@ in HBM.  Envs are sharded across ranks with no collective on the step path (weak
 `--envs` envs per GPU, rank r owns the global envs [r*E, (r+1)*E)).
 
 Timing (the driver's contract): W untimed warm-up steps, then exactly K timed steps bracketed by
-a barrier + device synchronize on both sides, the max over ranks.  K > 256 steps are replayed from
+a barrier + device synchronize on both sides, the max over ranks (each rank's clock runs from the
+opening synchronize to the closing one).  The ranks' process group is gloo (barriers, the max)
+unless `--ctde` gathers over RCCL: a rank without a data exchange holds no RCCL communicator.  K > 256 steps are replayed from
 a hipGraph holding one launch per action tensor of the ring (`value`, `ms_per_step`: the whole-job
 rate without per-step host launch cost); short regions (the driver's K = 20) are launched eagerly
 (host launches run ahead of the GPU; a replayed graph's kernels measured slower there); HIP events recorded on the launch stream around that
@@ -167,9 +169,10 @@ def parse(argv=None):
                                 or os.environ.get("SWARM_BENCH_FORCE_GATHER") == "1")
         graph_long = a.steps > 256 and not a.no_graph and not gathering and not a.eval
         a.groups = pre.get("groups_graph", pre.get("groups", 1)) if graph_long else pre.get("groups", 1)
-        if not graph_long and int(os.environ.get("WORLD_SIZE", "1")) > 1:
-            # a multi-rank process also holds RCCL's stream: 2 group streams + the default stream +
-            # RCCL stay within GPU_MAX_HW_QUEUES = 4 (3 groups would make a fifth, sharing a queue)
+        if not graph_long and gathering and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            # a gathering rank also holds RCCL's streams and the gather's side stream: 2 group
+            # streams + the default stream + RCCL stay within GPU_MAX_HW_QUEUES = 4.  Ranks without
+            # the gather hold no RCCL communicator (main(): gloo) and keep the one-rank groups
             a.groups = min(a.groups, 2)
     if a.groups < 1:
         ap.error("--groups must be >= 1")
@@ -201,15 +204,24 @@ def max_over_ranks(values, world: int, device=None) -> list[float]:
     return [float(x) for x in t.cpu()]
 
 
+def pg_backend(ctde: bool, rehearsal: bool) -> str:
+    """Process-group backend of a multi-rank run: RCCL ("nccl") only for the CTDE gather on real
+    GPUs; gloo for the barriers and the max over ranks otherwise (and for the rehearsal)."""
+    return "nccl" if ctde and not rehearsal else "gloo"
+
+
 def _barrier_on(world: int) -> bool:
     if world > 1:
         return True
     import torch.distributed as dist
-    return os.environ.get("SWARM_BENCH_ONE_RANK_PG") == "1" and dist.is_initialized()
+    return os.environ.get("SWARM_BENCH_ONE_RANK_PG", "") in ("1", "nccl", "gloo") and dist.is_initialized()
 
 
 def timed_region(body, world: int, sync, spin=None, pre=None) -> float:
-    """Barrier + sync, run `body`, sync + barrier; wall seconds of this rank.  `spin`: an event
+    """Barrier + sync, run `body`, sync + barrier; wall seconds of this rank from the opening sync
+    to the closing sync (the caller takes the max over ranks: every rank starts after the common
+    barrier, so the max is the job's time; the closing barrier's own latency, ~25-40 us over gloo
+    and more over RCCL, is not step time: profiles/r06m_pg_backend_ab.jsonl).  `spin`: an event
     polled until it completes before the closing sync (diagnostic --spin-sync).  `pre`: run
     before the opening sync (the start events of the device-time bracket: their host cost would
     otherwise delay the region's first launch)."""
@@ -225,10 +237,11 @@ def timed_region(body, world: int, sync, spin=None, pre=None) -> float:
         while not spin.query():
             pass
     sync()
+    t1 = time.perf_counter()
     if _barrier_on(world):
         import torch.distributed as dist
         dist.barrier()
-    return time.perf_counter() - t0
+    return t1 - t0
 
 
 def gather_schedule(steps: int, every: int) -> list[int]:
@@ -376,14 +389,18 @@ def main(argv=None):
                 raise SystemExit(f"bench.py rank {rank}: {world} ranks need {world} GPUs (one per rank), "
                                  f"{torch.cuda.device_count()} visible")
             torch.cuda.set_device(local)
-        dist.init_process_group("gloo" if rehearsal else "nccl")
+        # RCCL only where the step path exchanges data (the CTDE global_state all-gather); otherwise
+        # the barriers and the max over ranks go over gloo: a process holding an RCCL communicator ran
+        # the driver's command 27.0-28.8 us per step against 24.5-25.2 without one (r06m, one-rank
+        # groups; RCCL's streams take hardware queues from the env groups)
+        dist.init_process_group(pg_backend(args.ctde, rehearsal))
     dev = torch.device("cuda", local if world > 1 and not rehearsal else 0)
     torch.cuda.set_device(dev)
     own_pg = False
     # SWARM_BENCH_ONE_RANK_PG=1 (diagnostic): a one-rank RCCL group whose barrier brackets the timed
     # region, so a one-GPU box sees the streams and queues a multi-rank process holds (the group
     # count rule below parse(): profiles/r06l_groups_rccl_ab.jsonl)
-    one_rank_pg = world == 1 and os.environ.get("SWARM_BENCH_ONE_RANK_PG") == "1"
+    one_rank_pg = world == 1 and os.environ.get("SWARM_BENCH_ONE_RANK_PG", "") in ("1", "nccl", "gloo")
     if world == 1 and (one_rank_pg or (os.environ.get("SWARM_BENCH_FORCE_GATHER") == "1" and args.ctde)) \
             and not dist.is_initialized():
         # the CTDE gather on one GPU: a one-rank RCCL group (its cost on the step)
@@ -391,7 +408,8 @@ def main(argv=None):
         with socket.socket() as so_:
             so_.bind(("127.0.0.1", 0))
             port = so_.getsockname()[1]
-        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        backend = "gloo" if one_rank_pg and os.environ["SWARM_BENCH_ONE_RANK_PG"] == "gloo" else "nccl"
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
         own_pg = True
 
     from swarm_marl_amd import VecSwarm
@@ -824,7 +842,8 @@ def main(argv=None):
                        "ctde_gather_every": args.gather_every if gatherer is not None else None,
                        "ctde_gathers_timed": (sum(1 for k in gatherer.gathered_steps if k >= gather_t0)
                                               if gatherer is not None else None),
-                       "ctde_gather_backend": gatherer.backend if gatherer is not None else None},
+                       "ctde_gather_backend": gatherer.backend if gatherer is not None else None,
+                       "dist_backend": dist.get_backend() if dist.is_initialized() else None},
             "roofline": roof,
             "env_done_fraction_last_step": done_frac,
             **({"rehearsal": f"{world} ranks sharing cuda:0 over gloo (SWARM_BENCH_REHEARSAL): the "

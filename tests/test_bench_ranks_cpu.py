@@ -122,6 +122,21 @@ def test_bench_args_presets():
     assert a.envs == 64
 
 
+def test_rank_process_group_and_groups(monkeypatch):
+    """A rank holds an RCCL communicator only for the CTDE gather (r06l / r06m: one in the process
+    slowed the driver's command by 10-15 %), and only a gathering rank drops to 2 env groups."""
+    import bench
+    assert bench.pg_backend(ctde=False, rehearsal=False) == "gloo"
+    assert bench.pg_backend(ctde=True, rehearsal=False) == "nccl"
+    assert bench.pg_backend(ctde=True, rehearsal=True) == "gloo"
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    args = ["--gpus", "4", "--steps", "20", "--warmup", "5"]
+    assert bench.parse(args).groups == bench.PRESETS["headline"]["groups"]
+    assert bench.parse(args + ["--config", "n256"]).groups == min(bench.PRESETS["n256"]["groups"], 2)
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    assert bench.parse(args[:0] + ["--steps", "20", "--config", "n256"]).groups == bench.PRESETS["n256"]["groups"]
+
+
 def _run_bench(args, env_extra, timeout=240):
     import subprocess
     import sys
