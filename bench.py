@@ -409,7 +409,10 @@ def main(argv=None):
             so_.bind(("127.0.0.1", 0))
             port = so_.getsockname()[1]
         backend = "gloo" if one_rank_pg and os.environ["SWARM_BENCH_ONE_RANK_PG"] == "gloo" else "nccl"
-        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        # SWARM_BENCH_PG_EAGER=1 (diagnostic): the RCCL communicator (and its streams) created here,
+        # before the env's group streams, instead of at the first collective
+        eager = {"device_id": dev} if backend == "nccl" and os.environ.get("SWARM_BENCH_PG_EAGER") == "1" else {}
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, **eager)
         own_pg = True
 
     from swarm_marl_amd import VecSwarm
