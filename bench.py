@@ -167,7 +167,7 @@ def parse(argv=None):
         # alternating runs (profiles/r04s_groups.txt; 4 groups 25.3-25.4, 1 group 29.2-29.3)
         gathering = a.ctde and (int(os.environ.get("WORLD_SIZE", "1")) > 1
                                 or os.environ.get("SWARM_BENCH_FORCE_GATHER") == "1")
-        graph_long = a.steps > 256 and not a.no_graph and not gathering and not a.eval
+        graph_long = a.steps > 256 and not a.no_graph and not a.eval and (not gathering or a.gather_every == a.ring)
         a.groups = pre.get("groups_graph", pre.get("groups", 1)) if graph_long else pre.get("groups", 1)
         if not graph_long and gathering and int(os.environ.get("WORLD_SIZE", "1")) > 1:
             # a gathering rank also holds RCCL's streams and the gather's side stream: 2 group
@@ -179,6 +179,7 @@ def parse(argv=None):
 
     if a.gather_every < 1:
         ap.error("--gather-every must be >= 1")
+    a.graph_gather = False  # set by main(): gathering run replaying graphs (two slot halves)
     if a.gs_slots < 1:
         ap.error("--gs-slots must be >= 1")
     return a
@@ -423,6 +424,14 @@ def main(argv=None):
     # up (tests/test_gpu_ctde.py drives this branch over RCCL on one GPU)
     gathering = args.ctde and (world > 1 or (os.environ.get("SWARM_BENCH_FORCE_GATHER") == "1"
                                              and dist.is_initialized()))
+    # a gathering run with a long timed region replays graphs too: two sets of ring-step segment
+    # graphs, each writing its own half of a 2 x ring slot global_state ring, and the gather of a
+    # segment's last slot issued between segment replays (overlapping the next segment; the segment
+    # after that, which rewrites the slot, waits for it)
+    args.graph_gather = (gathering and args.steps > 256 and not args.no_graph and not args.eval
+                         and not args.policy and args.gather_every == args.ring)
+    if args.graph_gather:
+        args.gs_slots = 2 * args.ring
     raw = {"num_drones": n}
     if args.no_term:
         raw.update(collision_radius=0.0, obstacle_radius=0.0, goal_radius=0.0)
@@ -543,24 +552,28 @@ def main(argv=None):
     # long regions, where the host's ~5 us per launch would otherwise matter
     # --eval launches eagerly: a captured swarm_eval_update would replay its capture-time update
     # index, so the records' update order and the update count would be wrong
-    use_graph = (not args.no_graph and gatherer is None and tracker is None
-                 and (args.steps > 256 or args.graph_short))
+    use_graph = args.graph_gather or (not args.no_graph and gatherer is None and tracker is None
+                                      and (args.steps > 256 or args.graph_short))
     reps, rem = divmod(args.steps, args.ring)
     if use_graph:
-        def capture(n_steps, k0=0):  # one graph of n_steps ring steps per group, on its group stream
+        def capture(n_steps, k0=0, slots=False):  # one graph of n_steps ring steps per group, on its group stream
             out = []
             for g in range(G):
                 gr = torch.cuda.CUDAGraph()
+
+                def seg():
+                    for k in range(k0, k0 + n_steps):
+                        if slots:  # step k writes global_state slot k mod 2 x ring (baked into the graph)
+                            vec.select_global_state_slot(k % args.gs_slots)
+                        env_step_group(g, k)
                 # thread_local: the RCCL watchdog thread of a multi-rank run keeps querying its events
                 if G == 1:
                     with torch.cuda.graph(gr, capture_error_mode="thread_local"):
-                        for k in range(k0, k0 + n_steps):
-                            env_step_group(0, k)
+                        seg()
                 else:
                     st = vec.group_streams[g]
                     with torch.cuda.stream(st), torch.cuda.graph(gr, stream=st, capture_error_mode="thread_local"):
-                        for k in range(k0, k0 + n_steps):
-                            env_step_group(g, k)
+                        seg()
                 out.append(gr)
             return out
         def capture_fused(n_steps):  # ONE graph holding every group's chain (fork / join inside)
@@ -581,15 +594,25 @@ def main(argv=None):
                     s0.wait_event(ev_j)
             return [gr]
 
-        fused = args.graph == "fused" and G > 1
-        graphs = capture(args.ring)
+        fused = args.graph == "fused" and G > 1 and not args.graph_gather
+        if args.graph_gather:
+            # the gatherer's step count must sit on a slot-ring boundary when segment replays start:
+            # untimed eager steps without gathers up to it
+            while gatherer.k % args.gs_slots:
+                gatherer.before_step(launch_streams)
+                env_step(gatherer.k)
+                gatherer.after_step(launch_streams, gather=False)
+            sync()
+            halves = [capture(args.ring, 0, slots=True), capture(args.ring, args.ring, slots=True)]
+            vec.select_global_state_slot(0)
+        graphs = capture(args.ring) if not args.graph_gather else halves[0]
         # short timed regions (the driver's K = 20) replay all K steps from one graph per group
         # (or one fused graph), so that the wall clock holds one graph launch per group; longer
         # ones replay ring segments plus a graph of the K % ring remainder
         head = max(0, min(args.eager_head, args.steps - 1)) if args.steps <= 256 and not fused else 0
         whole = (capture_fused(args.steps) if fused else capture(args.steps - head, head)) \
-            if args.steps <= 256 else None
-        tail = capture(rem) if rem and whole is None else None
+            if args.steps <= 256 and not args.graph_gather else None
+        tail = capture(rem) if rem and whole is None and not args.graph_gather else None
 
         def replay_all(gs):
             if G == 1 or len(gs) == 1:  # one group, or the fused graph (on group stream 0)
@@ -599,7 +622,19 @@ def main(argv=None):
             for g, st in enumerate(vec.group_streams):
                 with torch.cuda.stream(st):
                     gs[g].replay()
-        replay_all(graphs)  # untimed
+        def gather_segments(k0, n_seg):  # graph-gather mode: n_seg segment replays from timed step k0
+            for j in range(n_seg):
+                ks = range(k0 + j * args.ring, k0 + (j + 1) * args.ring)
+                # the group streams wait for the gathers of the slot half this segment rewrites
+                gatherer.before_steps(args.ring, launch_streams)
+                replay_all(halves[(gatherer.k // args.ring) % 2])
+                for k in ks:
+                    gatherer.after_step(launch_streams, gather=k in gathers)
+
+        if args.graph_gather:
+            gather_segments(-(1 << 30), 2)  # untimed, no gathers (k < 0): each half launched once
+        else:
+            replay_all(graphs)  # untimed
         if whole is not None:
             replay_all(whole)  # untimed: the timed region is not the graph's first launch
         sync()
@@ -611,7 +646,11 @@ def main(argv=None):
             if args.stagger_us > 0 and G > 1:  # diagnostic: start group 1 later (phase offset)
                 with torch.cuda.stream(vec.group_streams[1]):
                     torch.cuda._sleep(int(args.stagger_us * 2400))
-            if whole is not None:
+            if args.graph_gather:
+                gather_segments(0, reps)
+                for k in range(reps * args.ring, args.steps):  # the K mod ring remainder, eager
+                    step(k)
+            elif whole is not None:
                 for k in range(head):  # eager head: the first kernels start at once
                     env_step(k)
                 replay_all(whole)
@@ -626,6 +665,9 @@ def main(argv=None):
         timing = ((f"{head} eager step(s), then " if head else "") +
                   f"hipGraph replay of the {args.steps - head} steps (actions from a {args.ring}-tensor ring)"
                   if whole is not None else f"hipGraph replay of {args.ring}-step segments") + (
+            f", CTDE all-gather of each segment's last global_state slot between segment replays (a "
+            f"{args.gs_slots}-slot ring, segments alternating halves; the K mod {args.ring} remainder eager)"
+            if args.graph_gather else "") + (
             (f", {G} env groups on {G} HIP streams (" + ("one graph holding all groups" if fused and whole is not None
                                                         else "one graph per group") + ")") if G > 1 else "") + (
             f" (policy {args.policy} + env step per step)" if pol is not None else "") + (
@@ -678,7 +720,10 @@ def main(argv=None):
         fixed = None if gatherer is None else max(args.ring, int(args.device_warmup_ms * 5))
         while ((time.perf_counter() - t0) * 1e3 < args.device_warmup_ms if fixed is None
                else warm_steps < fixed):
-            if use_graph:
+            if args.graph_gather:
+                gather_segments(-(1 << 30), 1)
+                warm_steps += args.ring
+            elif use_graph:
                 if whole is not None and args.warm_graph == "whole":
                     replay_all(whole)
                     warm_steps += args.steps

@@ -96,6 +96,17 @@ class GlobalStateGather:
         self.select_slot(s)
         return s
 
+    def before_steps(self, n: int, streams=()) -> None:
+        """before_step for the next n steps launched as one unit (a replayed graph segment that
+        writes slots k .. k + n - 1 mod R, its slots baked in at capture): the streams wait for the
+        pending gather of every one of those slots.  Follow with n after_step calls."""
+        for i in range(n):
+            s = (self.k + i) % self.slots
+            if self.cuda and self.slot_pending[s]:
+                for st in streams:
+                    st.wait_event(self.slot_done[s])
+                self.slot_pending[s] = False
+
     def after_step(self, streams=(), gather: bool = False) -> None:
         """Called after step k's launches were issued on `streams`; gathers its slot if asked."""
         s = self.k % self.slots

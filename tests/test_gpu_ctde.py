@@ -86,6 +86,74 @@ def test_overlapped_gather_equals_synchronous(pg, e, n, groups, slots, every):
     assert torch.equal(a.obs, b.obs) and torch.equal(a.pos, b.pos)
 
 
+@pytest.mark.parametrize("groups", [2, 4])
+def test_graph_segment_gather_equals_synchronous(pg, groups):
+    """bench.py's graph-replayed gathering run: per group, two hipGraphs of `ring` steps, each with
+    its global_state slots (one half of a 2 x ring ring) baked in at capture; a segment replay is
+    followed by the gather of its last slot (GlobalStateGather.before_steps / after_step), which
+    overlaps the next segment.  Every gather equals a synchronous run's, bit for bit."""
+    from swarm_marl_amd import VecSwarm
+    from swarm_marl_amd.distributed import GlobalStateGather, gather_global_state
+    dev = pg
+    e, n, ring, segs = 512, 64, 4, 7
+    kw = dict(device=dev, auto_reset=True, seed=33, with_global_state=True)
+    a = VecSwarm(e, {"num_drones": n}, groups=groups, global_state_slots=2 * ring, **kw)
+    b = VecSwarm(e, {"num_drones": n}, **kw)
+    a.reset()
+    b.reset()
+    acts = [_acts(dev, e, n, 700 + k) for k in range(ring)]
+    torch.cuda.synchronize()
+    halves = []
+    for h in range(2):
+        gs = []
+        for gi, st in enumerate(a.group_streams):
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(st), torch.cuda.graph(gr, stream=st, capture_error_mode="thread_local"):
+                for k in range(h * ring, (h + 1) * ring):
+                    a.select_global_state_slot(k % (2 * ring))
+                    a.step_group(gi, acts[k % ring])
+            gs.append(gr)
+        halves.append(gs)
+    torch.cuda.synchronize()  # capture runs nothing: a and b are still at the same reset state
+    g = GlobalStateGather(a.global_state_ring, a.select_global_state_slot, keep=segs)
+    start = torch.cuda.Event()
+    start.record(torch.cuda.current_stream(dev))
+    for st in a.group_streams:
+        st.wait_event(start)
+    ref = []
+    for j in range(segs):
+        g.before_steps(ring, a.group_streams)
+        for gi, st in enumerate(a.group_streams):
+            with torch.cuda.stream(st):
+                halves[(g.k // ring) % 2][gi].replay()
+        for i in range(ring):
+            g.after_step(a.group_streams, gather=i == ring - 1)
+        for i in range(ring):
+            b.step(acts[i])
+        ref.append(gather_global_state(b.global_state).clone())
+    a.join()
+    g.wait()
+    torch.cuda.synchronize()
+    assert g.gathered_steps == [ring * j + ring - 1 for j in range(segs)]
+    for j in range(segs):
+        assert torch.equal(g.result(j), ref[j]), f"gather after segment {j}"
+    assert torch.equal(a.obs, b.obs) and torch.equal(a.pos, b.pos)
+
+
+def test_bench_ctde_graph_gather_line_one_rank(pg, capsys):
+    """bench.main's graph-replayed gathering run (K > 256, --gather-every = --ring): the line
+    reports graph replay, 2 x ring slots and every scheduled gather inside the timed region."""
+    import bench
+    bench_args = ["--config", "n256", "--envs", "64", "--steps", "260", "--warmup", "3",
+                  "--device-warmup-ms", "1", "--no-cpu-baseline", "--cpu-variant-seconds", "0"]
+    rec = _run_main_with_world(bench, bench_args, capsys)
+    cfg = rec["config"]
+    assert cfg["ctde_allgather"] is True and cfg["ctde_gather_every"] == 8
+    assert cfg["ctde_gathers_timed"] == len(bench.gather_schedule(260, 8))
+    assert "hipGraph replay" in rec["step_timing"] and "16-slot ring" in rec["step_timing"]
+    assert rec["value"] > 0
+
+
 @pytest.mark.parametrize("mode", ["auto", "new"])
 def test_result_buffers_reused_after_consumer_reads(pg, mode):
     """keep=1 < gathers: every gather overwrites the previous one's buffer.  The consumer queues
