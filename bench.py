@@ -149,6 +149,11 @@ def parse(argv=None):
                     help="diagnostic: group 1's first timed step starts this much later (phase offset)")
     ap.add_argument("--gather-every", type=int, default=8,
                     help="CTDE all-gather period in steps (SURVEY.md §5: per batch, not per step)")
+    ap.add_argument("--graph-gather", action="store_true",
+                    help="CTDE gathering runs with K > 256 and --gather-every = --ring replay graphs of ring-step "
+                         "segments (two slot halves of a 2 x ring slot ring, the gather between segment replays); "
+                         "default eager: with an RCCL communicator in the process the replays ran slower "
+                         "(config 5: 42.3-45.4 vs 39.9 us per step, profiles/r06q_graph_gather_ab.jsonl)")
     ap.add_argument("--gs-slots", type=int, default=4,
                     help="CTDE global_state ring slots (multi-rank): a gathered slot is rewritten "
                          "only R steps later, so the gather overlaps R-1 steps")
@@ -167,7 +172,8 @@ def parse(argv=None):
         # alternating runs (profiles/r04s_groups.txt; 4 groups 25.3-25.4, 1 group 29.2-29.3)
         gathering = a.ctde and (int(os.environ.get("WORLD_SIZE", "1")) > 1
                                 or os.environ.get("SWARM_BENCH_FORCE_GATHER") == "1")
-        graph_long = a.steps > 256 and not a.no_graph and not a.eval and (not gathering or a.gather_every == a.ring)
+        graph_long = (a.steps > 256 and not a.no_graph and not a.eval
+                      and (not gathering or (a.graph_gather and a.gather_every == a.ring)))
         a.groups = pre.get("groups_graph", pre.get("groups", 1)) if graph_long else pre.get("groups", 1)
         if not graph_long and gathering and int(os.environ.get("WORLD_SIZE", "1")) > 1:
             # a gathering rank also holds RCCL's streams and the gather's side stream: 2 group
@@ -179,7 +185,6 @@ def parse(argv=None):
 
     if a.gather_every < 1:
         ap.error("--gather-every must be >= 1")
-    a.graph_gather = False  # set by main(): gathering run replaying graphs (two slot halves)
     if a.gs_slots < 1:
         ap.error("--gs-slots must be >= 1")
     return a
@@ -424,12 +429,12 @@ def main(argv=None):
     # up (tests/test_gpu_ctde.py drives this branch over RCCL on one GPU)
     gathering = args.ctde and (world > 1 or (os.environ.get("SWARM_BENCH_FORCE_GATHER") == "1"
                                              and dist.is_initialized()))
-    # a gathering run with a long timed region replays graphs too: two sets of ring-step segment
+    # --graph-gather: a gathering run with a long timed region replays graphs too: two sets of ring-step segment
     # graphs, each writing its own half of a 2 x ring slot global_state ring, and the gather of a
     # segment's last slot issued between segment replays (overlapping the next segment; the segment
     # after that, which rewrites the slot, waits for it)
-    args.graph_gather = (gathering and args.steps > 256 and not args.no_graph and not args.eval
-                         and not args.policy and args.gather_every == args.ring)
+    args.graph_gather = (args.graph_gather and gathering and args.steps > 256 and not args.no_graph
+                         and not args.eval and not args.policy and args.gather_every == args.ring)
     if args.graph_gather:
         args.gs_slots = 2 * args.ring
     raw = {"num_drones": n}

@@ -141,10 +141,10 @@ def test_graph_segment_gather_equals_synchronous(pg, groups):
 
 
 def test_bench_ctde_graph_gather_line_one_rank(pg, capsys):
-    """bench.main's graph-replayed gathering run (K > 256, --gather-every = --ring): the line
+    """bench.main's graph-replayed gathering run (--graph-gather, K > 256, --gather-every = --ring): the line
     reports graph replay, 2 x ring slots and every scheduled gather inside the timed region."""
     import bench
-    bench_args = ["--config", "n256", "--envs", "64", "--steps", "260", "--warmup", "3",
+    bench_args = ["--config", "n256", "--envs", "64", "--steps", "260", "--warmup", "3", "--graph-gather",
                   "--device-warmup-ms", "1", "--no-cpu-baseline", "--cpu-variant-seconds", "0"]
     rec = _run_main_with_world(bench, bench_args, capsys)
     cfg = rec["config"]
