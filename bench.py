@@ -19,8 +19,8 @@ in HBM.  Envs are sharded across ranks with no collective on the step path (weak
 Timing (the driver's contract): W untimed warm-up steps, then exactly K timed steps bracketed by
 a barrier + device synchronize on both sides, the max over ranks (each rank's clock runs from the
 opening synchronize to the closing one).  The ranks' process group is gloo (barriers, the max)
-unless `--ctde` gathers over RCCL: a rank without a data exchange holds no RCCL communicator.  K > 256 steps are replayed from
-a hipGraph holding one launch per action tensor of the ring (`value`, `ms_per_step`: the whole-job
+unless `--ctde` gathers over RCCL: a rank without a data exchange holds no RCCL communicator.
+K > 256 steps are replayed from a hipGraph holding one launch per action tensor of the ring (`value`, `ms_per_step`: the whole-job
 rate without per-step host launch cost); short regions (the driver's K = 20) are launched eagerly
 (host launches run ahead of the GPU; a replayed graph's kernels measured slower there); HIP events recorded on the launch stream around that
 timed region give the average launch duration (`roofline.kernel_ms_mean`, the roofline's time
@@ -398,14 +398,15 @@ def main(argv=None):
         # RCCL only where the step path exchanges data (the CTDE global_state all-gather); otherwise
         # the barriers and the max over ranks go over gloo: a process holding an RCCL communicator ran
         # the driver's command 27.0-28.8 us per step against 24.5-25.2 without one (r06m, one-rank
-        # groups; RCCL's streams take hardware queues from the env groups)
+        # groups; the launches reach and leave the queues more slowly, 8 hardware queues do not help:
+        # DESIGN.md §7, r06o-r06r)
         dist.init_process_group(pg_backend(args.ctde, rehearsal))
     dev = torch.device("cuda", local if world > 1 and not rehearsal else 0)
     torch.cuda.set_device(dev)
     own_pg = False
-    # SWARM_BENCH_ONE_RANK_PG=1 (diagnostic): a one-rank RCCL group whose barrier brackets the timed
-    # region, so a one-GPU box sees the streams and queues a multi-rank process holds (the group
-    # count rule below parse(): profiles/r06l_groups_rccl_ab.jsonl)
+    # SWARM_BENCH_ONE_RANK_PG=nccl|gloo (diagnostic; 1 = nccl): a one-rank process group whose barrier
+    # brackets the timed region, so a one-GPU box sees what a multi-rank process holds
+    # (profiles/r06l_groups_rccl_ab.jsonl, r06m / r06n_pg_backend_ab.jsonl)
     one_rank_pg = world == 1 and os.environ.get("SWARM_BENCH_ONE_RANK_PG", "") in ("1", "nccl", "gloo")
     if world == 1 and (one_rank_pg or (os.environ.get("SWARM_BENCH_FORCE_GATHER") == "1" and args.ctde)) \
             and not dist.is_initialized():
