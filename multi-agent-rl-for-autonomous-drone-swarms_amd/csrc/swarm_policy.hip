@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "swarm_mi355x.h"
@@ -485,8 +486,11 @@ __device__ __forceinline__ void split8(const f32x16& a, int s, bool act, f16x8& 
     lo[2 * q] = l.x; lo[2 * q + 1] = l.y;
   }
 }
+// soff is wave-uniform; readfirstlane says so to the compiler, which otherwise may compute it in a
+// VGPR and wrap the load in a waterfall loop (policy_mlp_x3l did: 23 loops per tile)
 __device__ __forceinline__ f16x8 wlo_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
+  return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                       r, (int)voff, __builtin_amdgcn_readfirstlane((int)soff), 0));
 }
 // hi*hi into c, both cross terms (scaled by 2^11) into x: a dependent 32x32x16 MFMA issues back to
 // back on gfx950 (MI355X_MICROARCH.md: one accumulator chain runs at the full 32 cycles per MFMA),
@@ -733,6 +737,171 @@ policy_mlp_x3(const FwdArgs A) {
   }
 }
 
+// f32x3 at two waves per SIMD (8 per workgroup, <= 256 registers each): policy_mlp_x3's arithmetic
+// in the same order — every accumulator sees the same MFMA sequence and the same epilogues, so the
+// outputs are bit-identical — without its one-wave latency hiding (epilogues interleaved into the
+// next block's MFMAs, double-buffered W2 lo batches, the next tile's observations requested early):
+// the SIMD's second wave fills those gaps instead, and the registers they held (~490 -> ~250) buy
+// that second wave.  Live across layer 2: h1 hi / lo (128), one layer-2 accumulator pair (32), the
+// fused layer-3 pair (32) and one k-step's W hi / lo fragments.
+#ifndef X3L_GROUP
+#define X3L_GROUP 2  // layer-2 k-steps between scheduling barriers
+#endif
+#ifndef X3L_AHEAD
+#define X3L_AHEAD 1  // W2 lo fragments in flight ahead of their MFMAs (divides 16; 2 / 4 / 8 no faster, r06u)
+#endif
+template <int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVES / 4 > 0 ? WAVES / 4 : 1)))
+policy_mlp_x3l(const FwdArgs A) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const Bf16Layout L(A.out);
+  {  // stage the hi blob in LDS, once per workgroup (as policy_mlp_x3)
+    const int4* src = reinterpret_cast<const int4*>(A.w);
+    int4* dst = reinterpret_cast<int4*>(lds);
+    const int n16 = (int)(L.total / 16);
+    constexpr int UNR = 4, STRIDE = 64 * WAVES;
+    for (int base = threadIdx.x; base < n16; base += STRIDE * UNR) {
+      int4 v[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int i = base + u * STRIDE;
+        v[u] = src[i < n16 ? i : n16 - 1];
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int i = base + u * STRIDE;
+        if (i < n16) dst[i] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t WL = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char*>(reinterpret_cast<const unsigned char*>(A.w) + L.total), 0, (int)L.total, BUF_DWORD3);
+  const int wave = threadIdx.x >> 6;
+  const long long ntiles = (A.rows + 31) / 32;
+  const float* b2 = reinterpret_cast<const float*>(lds + L.b2);
+  const float* b3 = reinterpret_cast<const float*>(lds + L.b3);
+  for (long long tile = (long long)blockIdx.x * WAVES + wave; tile < ntiles; tile += (long long)gridDim.x * WAVES) {
+    int lane = threadIdx.x & 63, in_r = A.in, out_r = A.out;
+    uint32_t sb = 0;
+    asm volatile("" : "+v"(lane), "+s"(in_r), "+s"(out_r), "+s"(sb));
+    const int in = in_r, out = out_r;
+    const int n = lane & 31, h = (lane >> 5) & 1;
+    const bool w3lane = n < out;
+    const int w3idx = h * out + n;
+    const uint32_t lb = 16u * (uint32_t)lane;
+    const f16x8* w1f = reinterpret_cast<const f16x8*>(lds + L.w1 + lb);
+    const f16x8* w2f = reinterpret_cast<const f16x8*>(lds + L.w2 + lb);
+    const f16x8* w3f = reinterpret_cast<const f16x8*>(lds + L.w3);
+    const long long row = tile * 32 + n;
+    const bool valid = row < A.rows;
+    // ---- obs fragments, split: x[row][16 ks + 8 h + j], x[in] = 1 (bias column)
+    f16x8 xh[KS1], xl[KS1];
+    {
+      const float* xr = A.obs + (valid ? row : A.rows - 1) * in;
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const int k0 = 16 * ks + 8 * h + j, k1 = k0 + 1;
+          const float v0 = xr[k0 < in ? k0 : in - 1], v1 = xr[k1 < in ? k1 : in - 1];
+          const float x0 = k0 < in ? v0 : (k0 == in ? 1.f : 0.f);
+          const float x1 = k1 < in ? v1 : (k1 == in ? 1.f : 0.f);
+          const f16x2 hh = __builtin_convertvector((f32x2){x0, x1}, f16x2);
+          const f32x2 hb = __builtin_convertvector(hh, f32x2);
+          const f16x2 ll = __builtin_convertvector((f32x2){(x0 - hb.x) * X3_LO_SCALE, (x1 - hb.y) * X3_LO_SCALE}, f16x2);
+          xh[ks][j] = hh.x; xh[ks][j + 1] = hh.y;
+          xl[ks][j] = ll.x; xl[ks][j + 1] = ll.y;
+        }
+    }
+    // ---- layer 1: 256 x (in + 1), relu -> h1 hi / lo (two k-step fragments per out block)
+    f16x8 h1h[KS2], h1l[KS2];
+#pragma unroll
+    for (int ob = 0; ob < OB; ++ob) {
+      f32x16 acc = f32x16{}, accx = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks) {
+        const f16x8 wl = wlo_load(WL, lb, sb + (uint32_t)(L.w1 + (size_t)(ob * KS1 + ks) * FRAG));
+        mfma3(w1f[(ob * KS1 + ks) * 64], wl, xh[ks], xl[ks], acc, accx);
+      }
+      acc = x3_sum(acc, accx);
+      split8(acc, 0, true, h1h[2 * ob], h1l[2 * ob]);
+      split8(acc, 1, true, h1h[2 * ob + 1], h1l[2 * ob + 1]);
+      // h1 lo in AGPRs (MFMA B operands may come from AGPRs), as in policy_mlp_x3
+      asm volatile("" : "+a"(h1l[2 * ob]), "+a"(h1l[2 * ob + 1]));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- layer 2 (relu) fused with layer 3: each out block's two split fragments feed layer 3's
+    // k-steps 2ob, 2ob+1
+    f32x16 acc3, acc3x = f32x16{};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
+      acc3[i] = m < out ? b3[m] : 0.f;
+    }
+    // W2 lo fragments stream X3L_AHEAD k-steps ahead of their MFMAs, across out-block boundaries
+    // (fragment q = ob * 16 + ks of the 128; the requests past the last one re-read it)
+    f16x8 wlq[X3L_AHEAD];
+#pragma unroll
+    for (int j = 0; j < X3L_AHEAD; ++j) wlq[j] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)j * FRAG));
+#pragma unroll 1
+    for (int ob = 0; ob < OB; ++ob) {
+      f32x16 acc, accx = f32x16{};
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 b = *reinterpret_cast<const float4*>(b2 + ob * 32 + 8 * g + 4 * h);
+        acc[4 * g + 0] = b.x; acc[4 * g + 1] = b.y; acc[4 * g + 2] = b.z; acc[4 * g + 3] = b.w;
+      }
+#pragma unroll
+      for (int ks = 0; ks < KS2; ++ks) {
+        const f16x8 wl = wlq[ks % X3L_AHEAD];
+        const int q = ob * KS2 + ks + X3L_AHEAD;
+        wlq[ks % X3L_AHEAD] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)(q < OB * KS2 ? q : OB * KS2 - 1) * FRAG));
+        mfma3(w2f[(ob * KS2 + ks) * 64], wl, h1h[ks], h1l[ks], acc, accx);
+        // LDS reads in flight bounded (the scheduler would hoist all 16 k-steps' W hi reads)
+        if (ks % X3L_GROUP == X3L_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
+      }
+      acc = x3_sum(acc, accx);
+      f16x8 a0h = {}, a1h = {}, a0l = {}, a1l = {};  // lanes n >= out feed logits rows that are never read
+      if (w3lane) {  // this block's layer-3 fragments (k-steps 2ob, 2ob+1), the lo halves from L2
+        a0h = w3f[(2 * ob) * 2 * out + w3idx];
+        a1h = w3f[(2 * ob + 1) * 2 * out + w3idx];
+        a0l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob) * 2 * out * 16));
+        a1l = wlo_load(WL, 16u * (uint32_t)w3idx, sb + (uint32_t)(L.w3 + (size_t)(2 * ob + 1) * 2 * out * 16));
+      }
+      f16x8 h2h, h2l;
+      split8(acc, 0, true, h2h, h2l);
+      mfma3(a0h, a0l, h2h, h2l, acc3, acc3x);
+      split8(acc, 1, true, h2h, h2l);
+      mfma3(a1h, a1l, h2h, h2l, acc3, acc3x);
+    }
+    acc3 = x3_sum(acc3, acc3x);
+    // ---- outputs: lane holds logits m = (i&3) + 8(i>>2) + 4h of its row (out <= 12: i < 8)
+    if (A.logits && valid) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (m < out) A.logits[row * out + m] = acc3[i];
+      }
+    }
+    if (A.actions) {
+      float lg[12];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        lg[i] = acc3[i];
+        lg[4 + i] = __shfl_xor(acc3[i], 32);
+        lg[8 + i] = acc3[4 + i];
+      }
+      const int ad = out / 2;
+      if (h == 0 && valid) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+          if (k < ad) A.actions[row * ad + k] = lg[k];
+      }
+    }
+  }
+}
+
 // bf16: 8 waves per workgroup (one workgroup per CU: the LDS blob), one 32-row tile per wave (12 /
 // 16 waves and two tiles per wave measured slower)
 constexpr int BF16_TILES = 1;
@@ -743,6 +912,9 @@ constexpr int F32_WAVES = 4;
 // W2 lo batches and the next tile's observations need ~380 registers (at 2 waves per SIMD, 256,
 // it spills)
 constexpr int X3_WAVES = 4;
+// policy_mlp_x3l (two waves per SIMD) unless SWARM_POLICY_X3_PIPELINED=1 is set in the environment
+// (the one-wave pipelined kernel; same outputs bit for bit)
+constexpr int X3L_WAVES = 8;
 
 thread_local char g_perr[256] = "";
 int pfail(int code, const char* msg) {
@@ -910,12 +1082,15 @@ int swarm_policy_forward(const swarm_policy_t* p, const float* obs, long long ro
     const int lds = (int)Bf16Layout(p->out_dim).total;
     const bool dflt = p->in_dim == 37 && p->out_dim == 6;
     (void)dflt;  // the compile-time-dims instance spills (71 VGPRs at 512); the runtime-dims one fits (492)
-    auto fn = policy_mlp_x3<X3_WAVES>;
+    const char* pipe = getenv("SWARM_POLICY_X3_PIPELINED");
+    const bool lean = !(pipe && pipe[0] == '1');
+    auto fn = lean ? policy_mlp_x3l<X3L_WAVES> : policy_mlp_x3<X3_WAVES>;
+    const int waves = lean ? X3L_WAVES : X3_WAVES;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
         hipSuccess)
       return pfail(SWARM_EHIP, "hipFuncSetAttribute failed");
-    const int grid = grid_for(X3_WAVES, (rows + 31) / 32);
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * X3_WAVES), lds, s, a);
+    const int grid = grid_for(waves, (rows + 31) / 32);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * waves), lds, s, a);
   } else {
     const int grid = grid_for(F32_WAVES, (rows + 15) / 16) * 2;
     hipLaunchKernelGGL(policy_mlp_f32<F32_WAVES>, dim3(grid), dim3(64 * F32_WAVES), 0, s, a);

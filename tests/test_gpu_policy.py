@@ -6,7 +6,8 @@ Oracle: the reference's exported actor graph (artifacts/policy.onnx, scripts/exp
 Tolerances (stated per path):
   f32  (v_mfma_f32_16x16x4_f32): |logit error| <= 1e-4 + 1e-5 |logit|  (summation order only)
   f32x3 (three v_mfma_f32_32x32x16_f16 passes over f16 hi / lo splits): the same bound; its host
-       emulation from the packed blob sits at 0.1 of it (tests/test_policy_cpu.py)
+       emulation from the packed blob sits at 0.1 of it (tests/test_policy_cpu.py); its two kernels
+       (two waves per SIMD, default; one wave pipelined) agree bit for bit
   bf16 (v_mfma_f32_32x32x16_bf16): within 0.02 of the NumPy emulation of the same bf16 arithmetic
        (tests/test_policy_cpu.py) and within 0.3 of the f32 graph (logits span about -37 .. 66).
 """
@@ -100,6 +101,24 @@ def test_headline_batch_f32_vs_float64(dev, fx):
     gotx3 = lgx3[idx].double().cpu().numpy()  # the three-pass f16 path meets the f32 tolerance
     assert np.all(np.abs(gotx3 - x) <= 1e-4 + 1e-5 * np.abs(x)), np.abs(gotx3 - x).max()
     assert np.abs(lg16[idx].double().cpu().numpy() - x).max() <= 0.3
+
+
+def test_x3_two_waves_equals_pipelined_bitwise(dev, fx, monkeypatch):
+    """policy_mlp_x3l (two waves per SIMD, the default f32x3 kernel) against policy_mlp_x3 (one
+    wave, pipelined; SWARM_POLICY_X3_PIPELINED=1): the same MFMA sequence per accumulator and the
+    same epilogues, so the logits agree bit for bit — full tiles, a ragged last tile, fewer rows
+    than one workgroup's waves, and more tiles than waves in the grid."""
+    layers, d = fx
+    pol = _pol(fx, dev, "f32x3")
+    g = torch.Generator(device=dev).manual_seed(11)
+    for rows in (1, 33, 255, 70_001):
+        obs = torch.randn((rows, 37), device=dev, generator=g) * 3
+        monkeypatch.setenv("SWARM_POLICY_X3_PIPELINED", "1")
+        ref = pol.logits(obs).clone()
+        monkeypatch.delenv("SWARM_POLICY_X3_PIPELINED")
+        got = pol.logits(obs)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref), (rows, (got - ref).abs().max().item())
 
 
 def test_sampled_actions(dev, fx):
