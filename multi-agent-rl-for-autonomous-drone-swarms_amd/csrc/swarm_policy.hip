@@ -854,9 +854,13 @@ policy_mlp_x3l(const FwdArgs A) {
       }
 #pragma unroll
       for (int ks = 0; ks < KS2; ++ks) {
+#ifdef X3L_DIAG_NOWLO  // diagnostic build only (wrong logits): W2 lo from the hi blob in LDS, no W2 lo stream
+        const f16x8 wl = w2f[(ob * KS2 + (ks ^ 1)) * 64];
+#else
         const f16x8 wl = wlq[ks % X3L_AHEAD];
         const int q = ob * KS2 + ks + X3L_AHEAD;
         wlq[ks % X3L_AHEAD] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)(q < OB * KS2 ? q : OB * KS2 - 1) * FRAG));
+#endif
         mfma3(w2f[(ob * KS2 + ks) * 64], wl, h1h[ks], h1l[ks], acc, accx);
         // LDS reads in flight bounded (the scheduler would hoist all 16 k-steps' W hi reads)
         if (ks % X3L_GROUP == X3L_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
