@@ -747,6 +747,9 @@ policy_mlp_x3(const FwdArgs A) {
 #ifndef X3L_GROUP
 #define X3L_GROUP 2  // layer-2 k-steps between scheduling barriers
 #endif
+#ifndef X3L_HI_AHEAD
+#define X3L_HI_AHEAD 1  // W2 hi read from LDS one k-step ahead
+#endif
 #ifndef X3L_AHEAD
 #define X3L_AHEAD 1  // W2 lo fragments in flight ahead of their MFMAs (divides 16; 2 / 4 / 8 no faster, r06u)
 #endif
@@ -852,8 +855,17 @@ policy_mlp_x3l(const FwdArgs A) {
         const float4 b = *reinterpret_cast<const float4*>(b2 + ob * 32 + 8 * g + 4 * h);
         acc[4 * g + 0] = b.x; acc[4 * g + 1] = b.y; acc[4 * g + 2] = b.z; acc[4 * g + 3] = b.w;
       }
+#if X3L_HI_AHEAD
+      f16x8 whq = w2f[(ob * KS2) * 64];  // W2 hi one k-step ahead of its MFMAs (LDS latency)
+#endif
 #pragma unroll
       for (int ks = 0; ks < KS2; ++ks) {
+#if X3L_HI_AHEAD
+        const f16x8 wh = whq;
+        if (ks + 1 < KS2) whq = w2f[(ob * KS2 + ks + 1) * 64];
+#else
+        const f16x8 wh = w2f[(ob * KS2 + ks) * 64];
+#endif
 #ifdef X3L_DIAG_NOWLO  // diagnostic build only (wrong logits): W2 lo from the hi blob in LDS, no W2 lo stream
         const f16x8 wl = w2f[(ob * KS2 + (ks ^ 1)) * 64];
 #else
@@ -861,7 +873,7 @@ policy_mlp_x3l(const FwdArgs A) {
         const int q = ob * KS2 + ks + X3L_AHEAD;
         wlq[ks % X3L_AHEAD] = wlo_load(WL, lb, sb + (uint32_t)(L.w2 + (size_t)(q < OB * KS2 ? q : OB * KS2 - 1) * FRAG));
 #endif
-        mfma3(w2f[(ob * KS2 + ks) * 64], wl, h1h[ks], h1l[ks], acc, accx);
+        mfma3(wh, wl, h1h[ks], h1l[ks], acc, accx);
         // LDS reads in flight bounded (the scheduler would hoist all 16 k-steps' W hi reads)
         if (ks % X3L_GROUP == X3L_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
       }
