@@ -852,7 +852,11 @@ def main(argv=None):
         if prof.get("valu_insts_per_launch"):
             roof["valu"] = valu_roofline(prof, kern_max)
             busy = roof["valu"].get("busy_frac")
-            if busy is not None and busy > roof["frac"]:
+            if pol is not None:  # rollout: the policy kernel (MFMA, the line's policy.roofline) holds most of the step
+                roof["bound"] = "mfma"
+                roof["bound_note"] = ("rollout step: the policy kernel (policy.roofline, MFMA) takes most of the step; "
+                                      "achieved / peak / unit / frac are the env step's HBM figures over the whole step")
+            elif busy is not None and busy > roof["frac"]:
                 if busy >= 0.5:
                     roof["bound"] = "valu"
                     roof["bound_note"] = ("the SIMDs' VALU issue (roofline.valu.busy_frac, class-costed) is busier "
